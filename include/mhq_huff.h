@@ -1,0 +1,113 @@
+/*
+ * mhq_huff.h -- C ABI of libmhq_huff.so, the MI355X (gfx950) batch codec for
+ * HPACK/QPACK Huffman string literals (RFC 7541 Appendix B).
+ *
+ * This is the drop-in boundary behind minhq's hc/huffman.go +
+ * hc/huffmantable.go.  The reference's streaming, one-literal surface
+ *   hc.NewHuffmanCompressor / (*HuffmanCompressor).Write / .Pad
+ *                                         (hc/huffman.go:18-37)
+ *   hc.NewHuffmanDecompressor / (*HuffmanDecompressor).Read
+ *                                         (hc/huffman.go:96-121)
+ * stays in Go; a cgo shim adds the batch entry points
+ *   hc.HuffmanEncodeBatch(lits [][]byte) [][]byte
+ *   hc.HuffmanDecodeBatch(enc  [][]byte) ([][]byte, []error)
+ * on top of the functions below.  Per literal the results are byte-for-byte
+ * those of Write+Pad and of Read-to-EOF respectively.
+ *
+ * Layout of a batch: n literals packed back to back; literal i is
+ * in[in_off[i] - in_off[0] .. in_off[i+1] - in_off[0]) for the host-memory
+ * entry points (in points at literal 0), and in[in_off[i] .. in_off[i+1]) for
+ * the device entry points.  Offsets are non-decreasing uint64 arrays of n+1
+ * entries.  Output regions follow the same convention with out_off.
+ *
+ * Ownership: every buffer is caller-owned and used only for the duration of
+ * the call (host entry points) or until the work on `stream` completes
+ * (device entry points).  The library never retains a caller pointer.
+ * Threading: every entry point may be called concurrently on one context.
+ * Errors: entry points return MHQ_OK (0) or a negative MHQ_E* code;
+ * mhq_strerror() gives its text.  Per-literal decode outcomes go to status[].
+ */
+#ifndef MHQ_HUFF_H
+#define MHQ_HUFF_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MHQ_OK 0
+#define MHQ_EINVAL (-22)  /* bad argument (null pointer, bad device index) */
+#define MHQ_ENOMEM (-12)  /* host or device allocation failed */
+#define MHQ_ENODEV (-19)  /* no usable gfx950 device */
+#define MHQ_EHIP (-1000)  /* a HIP runtime call failed: MHQ_EHIP - hipError_t */
+
+/* Per-literal decode status (status[] entries). */
+#define MHQ_LIT_OK 0      /* ran to the end of the literal (io.EOF), or the output region filled */
+#define MHQ_LIT_INVALID 1 /* errors.New("invalid Huffman coding"), hc/huffman.go:112 */
+
+typedef struct mhq_ctx mhq_ctx;
+
+/* Opens a context on `ndev` devices (0 = every visible device).  Builds the
+ * immutable code/decode tables once and uploads them to each device. */
+int mhq_open(mhq_ctx **out, int ndev);
+/* Same, on an explicit list of HIP device ordinals (one process per GPU:
+ * rank r opens {r}).  Context device index k is ordinals[k]. */
+int mhq_open_devices(mhq_ctx **out, const int *ordinals, int count);
+void mhq_close(mhq_ctx *ctx);
+int mhq_device_count(const mhq_ctx *ctx);
+const char *mhq_strerror(int rc);
+
+/* The 256-entry code table as the kernels use it (hc/huffmantable.go:9-267):
+ * len[s] bits, value code[s] right-justified.  For tests and tooling. */
+int mhq_code_table(uint8_t *len, uint32_t *code);
+
+/* ---------------- host-memory batches (PCIe-inclusive path) ---------------
+ * The batch is sharded over the context's devices by encoded bytes; each shard
+ * is copied in, processed and copied back.  Synchronous. */
+
+/* enc_len[i] = encoded bytes of literal i = ceil(sum of code lengths / 8).
+ * Replaces the sizing done by bytes.Buffer in hc/io.go:157-171; drives the
+ * Auto choice (hc/io.go:172: Huffman iff enc_len < raw length). */
+int mhq_huff_encode_len(mhq_ctx *ctx, const uint8_t *in, const uint64_t *in_off, uint64_t n,
+                        uint32_t *enc_len);
+
+/* HuffmanCompressor.Write + Pad per literal (hc/huffman.go:23-37): codes
+ * MSB-first, final octet padded with 1 bits.  out_off[i+1]-out_off[i] must be
+ * at least enc_len[i]; bytes past enc_len[i] in a region are unspecified. */
+int mhq_huff_encode(mhq_ctx *ctx, const uint8_t *in, const uint64_t *in_off, uint64_t n, uint8_t *out,
+                    const uint64_t *out_off);
+
+/* HuffmanDecompressor.Read until EOF per literal (hc/huffman.go:102-121),
+ * into a region of capacity out_off[i+1]-out_off[i] (floor(8*len/5) always
+ * suffices; hc/io.go:87 allocates len*8/5+1).  Writes out_len[i] and
+ * status[i].  Trailing partial codes (padding) are dropped without checks,
+ * as in the reference.  Bytes past out_len[i] in a region are unspecified. */
+int mhq_huff_decode(mhq_ctx *ctx, const uint8_t *in, const uint64_t *in_off, uint64_t n, uint8_t *out,
+                    const uint64_t *out_off, uint32_t *out_len, uint8_t *status);
+
+/* ---------------- device-resident batches ---------------------------------
+ * Same semantics; every pointer is device memory on device `dev` of the
+ * context; `stream` is a hipStream_t (NULL = the null stream).  Asynchronous:
+ * the call only enqueues work on `stream`. */
+int mhq_huff_encode_len_dev(mhq_ctx *ctx, int dev, const uint8_t *in, const uint64_t *in_off, uint64_t n,
+                            uint32_t *enc_len, void *stream);
+/* out_off[i] = base + sum_{j<i} enc_len[j] (n+1 entries) and, if cap_off is
+ * not NULL, cap_off[i] = cap_base + sum_{j<i} floor(8*enc_len[j]/5): the
+ * encode output offsets and the matching decode capacities. */
+int mhq_huff_offsets_dev(mhq_ctx *ctx, int dev, const uint32_t *enc_len, uint64_t n, uint64_t base,
+                         uint64_t *out_off, uint64_t *cap_off, void *stream);
+/* cap_off[i] = base + sum_{j<i} floor(8*(in_off[j+1]-in_off[j])/5). */
+int mhq_huff_capacity_dev(mhq_ctx *ctx, int dev, const uint64_t *in_off, uint64_t n, uint64_t base,
+                          uint64_t *cap_off, void *stream);
+int mhq_huff_encode_dev(mhq_ctx *ctx, int dev, const uint8_t *in, const uint64_t *in_off, uint64_t n,
+                        uint8_t *out, const uint64_t *out_off, void *stream);
+int mhq_huff_decode_dev(mhq_ctx *ctx, int dev, const uint8_t *in, const uint64_t *in_off, uint64_t n,
+                        uint8_t *out, const uint64_t *out_off, uint32_t *out_len, uint8_t *status,
+                        void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MHQ_HUFF_H */

@@ -1,0 +1,81 @@
+"""ctypes binding of libmhq_huff.so -- the same C ABI a cgo shim binds.
+
+Every symbol declared in include/mhq_huff.h is bound here with its exact
+signature.  There is no fallback: if the library is missing the import of
+any codec entry point raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libmhq_huff.so")
+
+MHQ_OK = 0
+MHQ_EINVAL = -22
+MHQ_ENOMEM = -12
+MHQ_ENODEV = -19
+MHQ_EHIP = -1000
+MHQ_LIT_OK = 0
+MHQ_LIT_INVALID = 1
+
+u8p = C.POINTER(C.c_uint8)
+u32p = C.POINTER(C.c_uint32)
+u64p = C.POINTER(C.c_uint64)
+vp = C.c_void_p
+
+# name -> (restype, argtypes); mirrors include/mhq_huff.h one to one.
+SIGNATURES = {
+    "mhq_open": (C.c_int, [C.POINTER(vp), C.c_int]),
+    "mhq_open_devices": (C.c_int, [C.POINTER(vp), C.POINTER(C.c_int), C.c_int]),
+    "mhq_close": (None, [vp]),
+    "mhq_device_count": (C.c_int, [vp]),
+    "mhq_strerror": (C.c_char_p, [C.c_int]),
+    "mhq_code_table": (C.c_int, [u8p, u32p]),
+    "mhq_huff_encode_len": (C.c_int, [vp, u8p, u64p, C.c_uint64, u32p]),
+    "mhq_huff_encode": (C.c_int, [vp, u8p, u64p, C.c_uint64, u8p, u64p]),
+    "mhq_huff_decode": (C.c_int, [vp, u8p, u64p, C.c_uint64, u8p, u64p, u32p, u8p]),
+    "mhq_huff_encode_len_dev": (C.c_int, [vp, C.c_int, vp, vp, C.c_uint64, vp, vp]),
+    "mhq_huff_offsets_dev": (C.c_int, [vp, C.c_int, vp, C.c_uint64, C.c_uint64, vp, vp, vp]),
+    "mhq_huff_capacity_dev": (C.c_int, [vp, C.c_int, vp, C.c_uint64, C.c_uint64, vp, vp]),
+    "mhq_huff_encode_dev": (C.c_int, [vp, C.c_int, vp, vp, C.c_uint64, vp, vp, vp]),
+    "mhq_huff_decode_dev": (C.c_int, [vp, C.c_int, vp, vp, C.c_uint64, vp, vp, vp, vp, vp]),
+}
+
+_lib = None
+
+
+class MhqError(RuntimeError):
+    def __init__(self, rc: int, what: str):
+        self.rc = rc
+        msg = _strerror(rc)
+        super().__init__(f"{what}: {msg} (rc={rc})")
+
+
+def _strerror(rc: int) -> str:
+    try:
+        return load().mhq_strerror(rc).decode()
+    except Exception:  # pragma: no cover
+        return "unknown"
+
+
+def load():
+    """Loads the in-tree libmhq_huff.so (raises OSError if it is absent)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise OSError(f"{LIB_PATH} is missing: run `python -m minhq_amd.build` "
+                          "(or __graft_entry__.build()) first")
+        L = C.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def check(rc: int, what: str) -> None:
+    if rc != MHQ_OK:
+        raise MhqError(rc, what)

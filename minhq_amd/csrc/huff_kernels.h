@@ -1,0 +1,36 @@
+// huff_kernels.h -- launchers for the gfx950 Huffman batch kernels.
+// Internal to libmhq_huff.so; the public surface is include/mhq_huff.h.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace mhq {
+
+// Device copies of the tables built by build_tables() (huff_table.h).
+struct DevTables {
+  const uint32_t *code;  // [256]
+  const uint8_t *len;    // [256]
+  const uint32_t *lut1;  // [kLut1Size]
+  const uint16_t *lut2;  // [kLut2Size]
+};
+
+// All offsets arrays have n+1 entries; literal i occupies
+// base[off[i] - bias .. off[i+1] - bias).
+hipError_t launch_encode_len(const DevTables &t, const uint8_t *in, const uint64_t *in_off,
+                             uint64_t in_bias, uint64_t n, uint32_t *enc_len, hipStream_t s);
+hipError_t launch_encode(const DevTables &t, const uint8_t *in, const uint64_t *in_off,
+                         uint64_t in_bias, uint64_t n, uint8_t *out, const uint64_t *out_off,
+                         uint64_t out_bias, hipStream_t s);
+hipError_t launch_decode(const DevTables &t, const uint8_t *in, const uint64_t *in_off,
+                         uint64_t in_bias, uint64_t n, uint8_t *out, const uint64_t *out_off,
+                         uint64_t out_bias, uint32_t *out_len, uint8_t *status, hipStream_t s);
+// out_off[i] = base + sum_{j<i} enc_len[j]; cap_off[i] = base + sum_{j<i} floor(8*enc_len[j]/5)
+// (either output may be null).  Scratch comes from hipMallocAsync on `s`.
+hipError_t launch_offsets(const uint32_t *enc_len, uint64_t n, uint64_t base, uint64_t *out_off,
+                          uint64_t *cap_off, hipStream_t s);
+// cap_off[i] = base + sum_{j<i} floor(8*(in_off[j+1]-in_off[j])/5): decode capacities
+// for a batch whose encoded offsets are known.
+hipError_t launch_capacity(const uint64_t *in_off, uint64_t n, uint64_t base, uint64_t *cap_off,
+                           hipStream_t s);
+
+}  // namespace mhq

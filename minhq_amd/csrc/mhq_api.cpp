@@ -1,0 +1,339 @@
+// mhq_api.cpp -- the C ABI of libmhq_huff.so (include/mhq_huff.h).
+//
+// Host-memory entry points shard the batch across the context's devices by
+// encoded bytes (literals are independent, no collective), run
+// H2D -> kernel -> D2H per shard on one host thread per device, and rebase the
+// offsets with a per-shard bias instead of rewriting them.  Device-resident
+// entry points only enqueue kernels on the caller's stream.
+#include <hip/hip_runtime.h>
+#include <string.h>
+
+#include <algorithm>
+#include <memory>
+#include <mutex>
+#include <thread>
+#include <vector>
+
+#include "../../include/mhq_huff.h"
+#include "huff_kernels.h"
+#include "huff_table.h"
+
+namespace {
+
+using mhq::DevTables;
+
+int hip_rc(hipError_t e) { return e == hipSuccess ? MHQ_OK : MHQ_EHIP - (int)e; }
+
+#define MHQ_TRY(expr)                        \
+  do {                                       \
+    hipError_t _e = (expr);                  \
+    if (_e != hipSuccess) return hip_rc(_e); \
+  } while (0)
+
+struct Buffer {
+  void *p = nullptr;
+  size_t cap = 0;
+  hipError_t reserve(size_t bytes) {
+    if (bytes <= cap) return hipSuccess;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+    size_t want = std::max<size_t>(bytes + bytes / 4, 1 << 16);
+    hipError_t e = hipMalloc(&p, want);
+    if (e == hipSuccess) cap = want;
+    return e;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+};
+
+struct Device {
+  int ordinal = 0;
+  void *table_mem = nullptr;
+  DevTables tables{};
+  std::mutex mu;  // serialises host-memory calls (they share the staging buffers)
+  hipStream_t stream = nullptr;
+  Buffer in, in_off, out, out_off, lens, status;
+};
+
+}  // namespace
+
+struct mhq_ctx {
+  std::vector<std::unique_ptr<Device>> devs;
+};
+
+namespace {
+
+std::once_flag g_tables_once;
+mhq::Tables g_tables;
+bool g_tables_ok = false;
+
+const mhq::Tables *tables() {
+  std::call_once(g_tables_once, [] { g_tables_ok = mhq::build_tables(&g_tables); });
+  return g_tables_ok ? &g_tables : nullptr;
+}
+
+int init_device(Device *d, int ordinal) {
+  d->ordinal = ordinal;
+  MHQ_TRY(hipSetDevice(ordinal));
+  hipDeviceProp_t prop;
+  MHQ_TRY(hipGetDeviceProperties(&prop, ordinal));
+  if (strncmp(prop.gcnArchName, "gfx950", 6) != 0) return MHQ_ENODEV;
+  const mhq::Tables *t = tables();
+  if (!t) return MHQ_EINVAL;
+  const size_t sz = sizeof(t->code) + sizeof(t->len) + sizeof(t->lut1) + sizeof(t->lut2);
+  MHQ_TRY(hipMalloc(&d->table_mem, sz));
+  uint8_t *base = (uint8_t *)d->table_mem;
+  // layout: lut1 | code | lut2 | len  (each naturally aligned)
+  uint8_t *p_lut1 = base;
+  uint8_t *p_code = p_lut1 + sizeof(t->lut1);
+  uint8_t *p_lut2 = p_code + sizeof(t->code);
+  uint8_t *p_len = p_lut2 + sizeof(t->lut2);
+  MHQ_TRY(hipMemcpy(p_lut1, t->lut1, sizeof(t->lut1), hipMemcpyHostToDevice));
+  MHQ_TRY(hipMemcpy(p_code, t->code, sizeof(t->code), hipMemcpyHostToDevice));
+  MHQ_TRY(hipMemcpy(p_lut2, t->lut2, sizeof(t->lut2), hipMemcpyHostToDevice));
+  MHQ_TRY(hipMemcpy(p_len, t->len, sizeof(t->len), hipMemcpyHostToDevice));
+  d->tables.lut1 = (const uint32_t *)p_lut1;
+  d->tables.code = (const uint32_t *)p_code;
+  d->tables.lut2 = (const uint16_t *)p_lut2;
+  d->tables.len = (const uint8_t *)p_len;
+  MHQ_TRY(hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking));
+  return MHQ_OK;
+}
+
+void free_device(Device *d) {
+  (void)hipSetDevice(d->ordinal);
+  d->in.release();
+  d->in_off.release();
+  d->out.release();
+  d->out_off.release();
+  d->lens.release();
+  d->status.release();
+  if (d->stream) (void)hipStreamDestroy(d->stream);
+  if (d->table_mem) (void)hipFree(d->table_mem);
+}
+
+Device *device(mhq_ctx *ctx, int dev) {
+  if (!ctx || dev < 0 || dev >= (int)ctx->devs.size()) return nullptr;
+  return ctx->devs[dev].get();
+}
+
+// Splits [0,n) into ctx->devs.size() contiguous shards of near-equal bytes.
+std::vector<uint64_t> shard_bounds(const uint64_t *off, uint64_t n, size_t parts) {
+  std::vector<uint64_t> b(parts + 1, n);
+  b[0] = 0;
+  const uint64_t total = off[n] - off[0];
+  for (size_t k = 1; k < parts; k++) {
+    const uint64_t target = off[0] + (uint64_t)((unsigned __int128)total * k / parts);
+    b[k] = (uint64_t)(std::lower_bound(off, off + n, target) - off);
+    b[k] = std::max(b[k], b[k - 1]);
+  }
+  return b;
+}
+
+enum class Op { kEncodeLen, kEncode, kDecode };
+
+struct HostJob {
+  Op op;
+  const uint8_t *in;
+  const uint64_t *in_off;
+  uint8_t *out;
+  const uint64_t *out_off;
+  uint32_t *lens;
+  uint8_t *status;
+};
+
+// Runs literals [a, b) of a host-memory job on one device.
+int run_shard(Device *d, const HostJob &j, uint64_t a, uint64_t b) {
+  const uint64_t m = b - a;
+  if (m == 0) return MHQ_OK;
+  std::lock_guard<std::mutex> lock(d->mu);
+  MHQ_TRY(hipSetDevice(d->ordinal));
+  hipStream_t s = d->stream;
+  const uint64_t in_bias = j.in_off[a];
+  const uint64_t in_bytes = j.in_off[b] - j.in_off[a];
+  MHQ_TRY(d->in.reserve(in_bytes + 16));
+  MHQ_TRY(d->in_off.reserve((m + 1) * sizeof(uint64_t)));
+  MHQ_TRY(hipMemcpyAsync(d->in.p, j.in + (j.in_off[a] - j.in_off[0]), in_bytes, hipMemcpyHostToDevice, s));
+  MHQ_TRY(hipMemcpyAsync(d->in_off.p, j.in_off + a, (m + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, s));
+  const uint8_t *din = (const uint8_t *)d->in.p;
+  const uint64_t *din_off = (const uint64_t *)d->in_off.p;
+  if (j.op == Op::kEncodeLen) {
+    MHQ_TRY(d->lens.reserve(m * sizeof(uint32_t)));
+    MHQ_TRY(mhq::launch_encode_len(d->tables, din, din_off, in_bias, m, (uint32_t *)d->lens.p, s));
+    MHQ_TRY(hipMemcpyAsync(j.lens + a, d->lens.p, m * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    return hip_rc(hipStreamSynchronize(s));
+  }
+  const uint64_t out_bias = j.out_off[a];
+  const uint64_t out_bytes = j.out_off[b] - j.out_off[a];
+  MHQ_TRY(d->out.reserve(out_bytes + 16));
+  MHQ_TRY(d->out_off.reserve((m + 1) * sizeof(uint64_t)));
+  MHQ_TRY(hipMemcpyAsync(d->out_off.p, j.out_off + a, (m + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, s));
+  // Regions are fully defined on return: unspecified bytes come back as zeros.
+  MHQ_TRY(hipMemsetAsync(d->out.p, 0, out_bytes, s));
+  uint8_t *dout = (uint8_t *)d->out.p;
+  const uint64_t *dout_off = (const uint64_t *)d->out_off.p;
+  if (j.op == Op::kEncode) {
+    MHQ_TRY(mhq::launch_encode(d->tables, din, din_off, in_bias, m, dout, dout_off, out_bias, s));
+  } else {
+    MHQ_TRY(d->lens.reserve(m * sizeof(uint32_t)));
+    MHQ_TRY(d->status.reserve(m));
+    MHQ_TRY(mhq::launch_decode(d->tables, din, din_off, in_bias, m, dout, dout_off, out_bias,
+                               (uint32_t *)d->lens.p, (uint8_t *)d->status.p, s));
+    MHQ_TRY(hipMemcpyAsync(j.lens + a, d->lens.p, m * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    MHQ_TRY(hipMemcpyAsync(j.status + a, d->status.p, m, hipMemcpyDeviceToHost, s));
+  }
+  MHQ_TRY(hipMemcpyAsync(j.out + (j.out_off[a] - j.out_off[0]), dout, out_bytes, hipMemcpyDeviceToHost, s));
+  return hip_rc(hipStreamSynchronize(s));
+}
+
+int run_host(mhq_ctx *ctx, const HostJob &j, uint64_t n) {
+  if (!ctx || ctx->devs.empty()) return MHQ_EINVAL;
+  if (n == 0) return MHQ_OK;
+  if (!j.in_off || (!j.in && j.in_off[n] != j.in_off[0])) return MHQ_EINVAL;
+  const size_t D = ctx->devs.size();
+  std::vector<uint64_t> b = shard_bounds(j.in_off, n, D);
+  if (D == 1) return run_shard(ctx->devs[0].get(), j, 0, n);
+  std::vector<int> rc(D, MHQ_OK);
+  std::vector<std::thread> th;
+  for (size_t k = 0; k < D; k++)
+    th.emplace_back([&, k] { rc[k] = run_shard(ctx->devs[k].get(), j, b[k], b[k + 1]); });
+  for (auto &t : th) t.join();
+  for (int r : rc)
+    if (r != MHQ_OK) return r;
+  return MHQ_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int mhq_open(mhq_ctx **out, int ndev) {
+  if (!out) return MHQ_EINVAL;
+  *out = nullptr;
+  int count = 0;
+  hipError_t e = hipGetDeviceCount(&count);
+  if (e != hipSuccess || count == 0) return MHQ_ENODEV;
+  if (ndev <= 0 || ndev > count) ndev = count;
+  std::vector<int> ord(ndev);
+  for (int i = 0; i < ndev; i++) ord[i] = i;
+  return mhq_open_devices(out, ord.data(), ndev);
+}
+
+int mhq_open_devices(mhq_ctx **out, const int *ordinals, int ndev) {
+  if (!out || !ordinals || ndev <= 0) return MHQ_EINVAL;
+  *out = nullptr;
+  int count = 0;
+  hipError_t e = hipGetDeviceCount(&count);
+  if (e != hipSuccess || count == 0) return MHQ_ENODEV;
+  auto ctx = std::make_unique<mhq_ctx>();
+  for (int i = 0; i < ndev; i++) {
+    if (ordinals[i] < 0 || ordinals[i] >= count) {
+      for (auto &x : ctx->devs) free_device(x.get());
+      return MHQ_EINVAL;
+    }
+    auto d = std::make_unique<Device>();
+    int rc = init_device(d.get(), ordinals[i]);
+    if (rc != MHQ_OK) {
+      free_device(d.get());
+      for (auto &x : ctx->devs) free_device(x.get());
+      return rc;
+    }
+    ctx->devs.push_back(std::move(d));
+  }
+  *out = ctx.release();
+  return MHQ_OK;
+}
+
+void mhq_close(mhq_ctx *ctx) {
+  if (!ctx) return;
+  for (auto &d : ctx->devs) free_device(d.get());
+  delete ctx;
+}
+
+int mhq_device_count(const mhq_ctx *ctx) { return ctx ? (int)ctx->devs.size() : 0; }
+
+const char *mhq_strerror(int rc) {
+  switch (rc) {
+    case MHQ_OK: return "ok";
+    case MHQ_EINVAL: return "invalid argument";
+    case MHQ_ENOMEM: return "out of memory";
+    case MHQ_ENODEV: return "no gfx950 (MI355X) device available";
+    default:
+      if (rc <= MHQ_EHIP) return hipGetErrorString((hipError_t)(MHQ_EHIP - rc));
+      return "unknown error";
+  }
+}
+
+int mhq_code_table(uint8_t *len, uint32_t *code) {
+  const mhq::Tables *t = tables();
+  if (!t || !len || !code) return MHQ_EINVAL;
+  memcpy(len, t->len, sizeof(t->len));
+  memcpy(code, t->code, sizeof(t->code));
+  return MHQ_OK;
+}
+
+int mhq_huff_encode_len(mhq_ctx *ctx, const uint8_t *in, const uint64_t *in_off, uint64_t n,
+                        uint32_t *enc_len) {
+  if (n && !enc_len) return MHQ_EINVAL;
+  return run_host(ctx, HostJob{Op::kEncodeLen, in, in_off, nullptr, nullptr, enc_len, nullptr}, n);
+}
+
+int mhq_huff_encode(mhq_ctx *ctx, const uint8_t *in, const uint64_t *in_off, uint64_t n, uint8_t *out,
+                    const uint64_t *out_off) {
+  if (n && (!out_off || (!out && out_off[n] != out_off[0]))) return MHQ_EINVAL;
+  return run_host(ctx, HostJob{Op::kEncode, in, in_off, out, out_off, nullptr, nullptr}, n);
+}
+
+int mhq_huff_decode(mhq_ctx *ctx, const uint8_t *in, const uint64_t *in_off, uint64_t n, uint8_t *out,
+                    const uint64_t *out_off, uint32_t *out_len, uint8_t *status) {
+  if (n && (!out_off || !out_len || !status || (!out && out_off[n] != out_off[0]))) return MHQ_EINVAL;
+  return run_host(ctx, HostJob{Op::kDecode, in, in_off, out, out_off, out_len, status}, n);
+}
+
+int mhq_huff_encode_len_dev(mhq_ctx *ctx, int dev, const uint8_t *in, const uint64_t *in_off, uint64_t n,
+                            uint32_t *enc_len, void *stream) {
+  Device *d = device(ctx, dev);
+  if (!d || (n && (!in_off || !enc_len))) return MHQ_EINVAL;
+  MHQ_TRY(hipSetDevice(d->ordinal));
+  return hip_rc(mhq::launch_encode_len(d->tables, in, in_off, 0, n, enc_len, (hipStream_t)stream));
+}
+
+int mhq_huff_offsets_dev(mhq_ctx *ctx, int dev, const uint32_t *enc_len, uint64_t n, uint64_t base,
+                         uint64_t *out_off, uint64_t *cap_off, void *stream) {
+  Device *d = device(ctx, dev);
+  if (!d || !out_off || (n && !enc_len)) return MHQ_EINVAL;
+  MHQ_TRY(hipSetDevice(d->ordinal));
+  return hip_rc(mhq::launch_offsets(enc_len, n, base, out_off, cap_off, (hipStream_t)stream));
+}
+
+int mhq_huff_capacity_dev(mhq_ctx *ctx, int dev, const uint64_t *in_off, uint64_t n, uint64_t base,
+                          uint64_t *cap_off, void *stream) {
+  Device *d = device(ctx, dev);
+  if (!d || !cap_off || !in_off) return MHQ_EINVAL;
+  MHQ_TRY(hipSetDevice(d->ordinal));
+  return hip_rc(mhq::launch_capacity(in_off, n, base, cap_off, (hipStream_t)stream));
+}
+
+int mhq_huff_encode_dev(mhq_ctx *ctx, int dev, const uint8_t *in, const uint64_t *in_off, uint64_t n,
+                        uint8_t *out, const uint64_t *out_off, void *stream) {
+  Device *d = device(ctx, dev);
+  if (!d || (n && (!in_off || !out_off))) return MHQ_EINVAL;
+  MHQ_TRY(hipSetDevice(d->ordinal));
+  return hip_rc(mhq::launch_encode(d->tables, in, in_off, 0, n, out, out_off, 0, (hipStream_t)stream));
+}
+
+int mhq_huff_decode_dev(mhq_ctx *ctx, int dev, const uint8_t *in, const uint64_t *in_off, uint64_t n,
+                        uint8_t *out, const uint64_t *out_off, uint32_t *out_len, uint8_t *status,
+                        void *stream) {
+  Device *d = device(ctx, dev);
+  if (!d || (n && (!in_off || !out_off || !out_len || !status))) return MHQ_EINVAL;
+  MHQ_TRY(hipSetDevice(d->ordinal));
+  return hip_rc(mhq::launch_decode(d->tables, in, in_off, 0, n, out, out_off, 0, out_len, status,
+                                   (hipStream_t)stream));
+}
+
+}  // extern "C"

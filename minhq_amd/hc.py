@@ -1,0 +1,247 @@
+"""Host-side mirror of minhq's `hc` Huffman surface over the HIP C ABI.
+
+The reference's streaming API (hc/huffman.go:11-121) is one literal at a time
+and stays in Go; what this build adds behind it is the batch path that the
+cgo shim in INTEGRATION.md exposes as
+
+    hc.HuffmanEncodeBatch(lits [][]byte) [][]byte
+    hc.HuffmanDecodeBatch(enc  [][]byte) ([][]byte, []error)
+
+This module is that shim's Python twin (ctypes instead of cgo), so the parity
+tests drive the library exactly as Go would: pack literals into one byte
+buffer plus uint64 offsets, call the C ABI, unpack.  Names, argument meaning
+and error behaviour follow the reference:
+
+* HuffmanEncodeBatch(lits)[i] == Write(lits[i]) + Pad()   (hc/huffman.go:23-37)
+* HuffmanDecodeBatch(enc)[i]  == Read to EOF of enc[i]    (hc/huffman.go:102-121);
+  an invalid code gives the bytes produced so far and
+  InvalidHuffmanCoding("invalid Huffman coding") (hc/huffman.go:112).
+* HuffmanCodingAuto/Always/Never and the strictly-shorter Auto rule
+  (hc/io.go:140-150, :172) are exposed for callers that frame literals.
+
+There is no CPU fallback: every entry point runs on the gfx950 library and
+raises if it cannot.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from . import _lib
+from ._lib import check
+
+# hc/io.go:140-150
+HuffmanCodingAuto = 0
+HuffmanCodingAlways = 1
+HuffmanCodingNever = 2
+
+
+class InvalidHuffmanCoding(ValueError):
+    """errors.New("invalid Huffman coding") -- hc/huffman.go:112."""
+
+    def __init__(self):
+        super().__init__("invalid Huffman coding")
+
+
+def pack(lits: Sequence[bytes]) -> Tuple[np.ndarray, np.ndarray]:
+    """Packs literals back to back; returns (bytes u8[], offsets u64[n+1])."""
+    off = np.zeros(len(lits) + 1, dtype=np.uint64)
+    if lits:
+        off[1:] = np.cumsum([len(x) for x in lits], dtype=np.uint64)
+    data = np.frombuffer(b"".join(lits), dtype=np.uint8) if lits else np.zeros(0, np.uint8)
+    return np.ascontiguousarray(data), off
+
+
+def unpack(data: np.ndarray, off: np.ndarray, lens: Optional[np.ndarray] = None) -> List[bytes]:
+    buf = data.tobytes()
+    base = int(off[0]) if len(off) else 0
+    out = []
+    for i in range(len(off) - 1):
+        a = int(off[i]) - base
+        b = a + int(lens[i]) if lens is not None else int(off[i + 1]) - base
+        out.append(buf[a:b])
+    return out
+
+
+def capacity_offsets(enc_off: np.ndarray) -> np.ndarray:
+    """cap_off for decode: floor(8*len/5) per literal (hc/io.go:87 allocates one more)."""
+    lens = np.diff(enc_off.astype(np.uint64))
+    cap = np.zeros(len(enc_off), dtype=np.uint64)
+    if len(lens):
+        cap[1:] = np.cumsum(lens * np.uint64(8) // np.uint64(5), dtype=np.uint64)
+    return cap
+
+
+def _p(a: np.ndarray, t):
+    return a.ctypes.data_as(C.POINTER(t))
+
+
+def _nonempty(a: np.ndarray) -> np.ndarray:
+    # ctypes needs a valid pointer even for zero-length buffers
+    return a if a.size else np.zeros(1, dtype=a.dtype)
+
+
+class Codec:
+    """An mhq_ctx: the device tables and staging buffers on `ndev` GPUs (0 = all),
+    or on the explicit HIP device ordinals `devices`."""
+
+    def __init__(self, ndev: int = 0, devices: Optional[Sequence[int]] = None):
+        self._L = _lib.load()
+        h = C.c_void_p()
+        if devices is not None:
+            arr = (C.c_int * len(devices))(*devices)
+            check(self._L.mhq_open_devices(C.byref(h), arr, len(devices)), "mhq_open_devices")
+        else:
+            check(self._L.mhq_open(C.byref(h), ndev), "mhq_open")
+        self._h = h
+
+    @property
+    def handle(self):
+        return self._h
+
+    @property
+    def ndev(self) -> int:
+        return self._L.mhq_device_count(self._h)
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            self._L.mhq_close(self._h)
+            self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---------------- host-memory batches ----------------
+    def encode_len(self, data: np.ndarray, off: np.ndarray) -> np.ndarray:
+        n = len(off) - 1
+        out = np.zeros(max(n, 1), dtype=np.uint32)
+        data = _nonempty(np.ascontiguousarray(data, dtype=np.uint8))
+        off = np.ascontiguousarray(off, dtype=np.uint64)
+        check(self._L.mhq_huff_encode_len(self._h, _p(data, C.c_uint8), _p(off, C.c_uint64), n,
+                                          _p(out, C.c_uint32)), "mhq_huff_encode_len")
+        return out[:n]
+
+    def encode(self, data: np.ndarray, off: np.ndarray) -> Tuple[np.ndarray, np.ndarray]:
+        """Returns (encoded bytes, encoded offsets) for a packed batch."""
+        n = len(off) - 1
+        enc_len = self.encode_len(data, off)
+        enc_off = np.zeros(n + 1, dtype=np.uint64)
+        if n:
+            enc_off[1:] = np.cumsum(enc_len, dtype=np.uint64)
+        out = np.zeros(max(int(enc_off[-1]), 1), dtype=np.uint8)
+        data = _nonempty(np.ascontiguousarray(data, dtype=np.uint8))
+        off = np.ascontiguousarray(off, dtype=np.uint64)
+        check(self._L.mhq_huff_encode(self._h, _p(data, C.c_uint8), _p(off, C.c_uint64), n,
+                                      _p(out, C.c_uint8), _p(enc_off, C.c_uint64)), "mhq_huff_encode")
+        return out[: int(enc_off[-1])], enc_off
+
+    def decode(self, enc: np.ndarray, off: np.ndarray, cap_off: Optional[np.ndarray] = None):
+        """Returns (out, cap_off, out_len, status) for a packed batch."""
+        n = len(off) - 1
+        off = np.ascontiguousarray(off, dtype=np.uint64)
+        if cap_off is None:
+            cap_off = capacity_offsets(off)
+        cap_off = np.ascontiguousarray(cap_off, dtype=np.uint64)
+        out = np.zeros(max(int(cap_off[-1] - cap_off[0]) if n else 0, 1), dtype=np.uint8)
+        out_len = np.zeros(max(n, 1), dtype=np.uint32)
+        status = np.zeros(max(n, 1), dtype=np.uint8)
+        enc = _nonempty(np.ascontiguousarray(enc, dtype=np.uint8))
+        check(self._L.mhq_huff_decode(self._h, _p(enc, C.c_uint8), _p(off, C.c_uint64), n,
+                                      _p(out, C.c_uint8), _p(cap_off, C.c_uint64), _p(out_len, C.c_uint32),
+                                      _p(status, C.c_uint8)), "mhq_huff_decode")
+        return out, cap_off, out_len[:n], status[:n]
+
+    # ---------------- device-resident batches (torch tensors on one device) ---
+    @staticmethod
+    def _stream(stream):
+        if stream is None:
+            import torch
+
+            return C.c_void_p(torch.cuda.current_stream().cuda_stream)
+        return C.c_void_p(int(stream))
+
+    def encode_len_dev(self, data, off, enc_len, dev: int = 0, stream=None) -> None:
+        n = off.numel() - 1
+        check(self._L.mhq_huff_encode_len_dev(self._h, dev, data.data_ptr(), off.data_ptr(), n,
+                                              enc_len.data_ptr(), self._stream(stream)), "encode_len_dev")
+
+    def offsets_dev(self, enc_len, out_off, cap_off=None, base: int = 0, dev: int = 0, stream=None) -> None:
+        n = out_off.numel() - 1
+        check(self._L.mhq_huff_offsets_dev(self._h, dev, enc_len.data_ptr(), n, base, out_off.data_ptr(),
+                                           cap_off.data_ptr() if cap_off is not None else None,
+                                           self._stream(stream)), "offsets_dev")
+
+    def capacity_dev(self, in_off, cap_off, base: int = 0, dev: int = 0, stream=None) -> None:
+        n = in_off.numel() - 1
+        check(self._L.mhq_huff_capacity_dev(self._h, dev, in_off.data_ptr(), n, base, cap_off.data_ptr(),
+                                            self._stream(stream)), "capacity_dev")
+
+    def encode_dev(self, data, off, out, out_off, dev: int = 0, stream=None) -> None:
+        n = off.numel() - 1
+        check(self._L.mhq_huff_encode_dev(self._h, dev, data.data_ptr(), off.data_ptr(), n, out.data_ptr(),
+                                          out_off.data_ptr(), self._stream(stream)), "encode_dev")
+
+    def decode_dev(self, enc, off, out, cap_off, out_len, status, dev: int = 0, stream=None) -> None:
+        n = off.numel() - 1
+        check(self._L.mhq_huff_decode_dev(self._h, dev, enc.data_ptr(), off.data_ptr(), n, out.data_ptr(),
+                                          cap_off.data_ptr(), out_len.data_ptr(), status.data_ptr(),
+                                          self._stream(stream)), "decode_dev")
+
+
+_default: Optional[Codec] = None
+
+
+def default_codec() -> Codec:
+    global _default
+    if _default is None:
+        _default = Codec()
+    return _default
+
+
+def code_table() -> Tuple[List[int], List[int]]:
+    """The kernels' code table (hc/huffmantable.go:9-267) as (len[], code[])."""
+    L = _lib.load()
+    ln = (C.c_uint8 * 256)()
+    code = (C.c_uint32 * 256)()
+    check(L.mhq_code_table(ln, code), "mhq_code_table")
+    return list(ln), list(code)
+
+
+# ------------------------------------------------------------------------
+# The batch entry points the cgo shim adds to package hc.
+# ------------------------------------------------------------------------
+def HuffmanEncodeBatch(lits: Sequence[bytes], codec: Optional[Codec] = None) -> List[bytes]:
+    """Per literal: HuffmanCompressor.Write(l) then Pad() (hc/huffman.go:23-37)."""
+    codec = codec or default_codec()
+    data, off = pack(lits)
+    enc, enc_off = codec.encode(data, off)
+    return unpack(enc, enc_off)
+
+
+def HuffmanDecodeBatch(enc: Sequence[bytes], codec: Optional[Codec] = None
+                       ) -> Tuple[List[bytes], List[Optional[Exception]]]:
+    """Per literal: HuffmanDecompressor.Read until EOF (hc/huffman.go:102-121)."""
+    codec = codec or default_codec()
+    data, off = pack(enc)
+    out, cap_off, out_len, status = codec.decode(data, off)
+    vals = unpack(out, cap_off, out_len)
+    errs = [InvalidHuffmanCoding() if s == _lib.MHQ_LIT_INVALID else None for s in status]
+    return vals, errs
+
+
+def HuffmanChoose(raw_len: int, enc_len: int, choice: int = HuffmanCodingAuto) -> bool:
+    """Whether WriteStringRaw sends the Huffman form (hc/io.go:156-178)."""
+    if choice == HuffmanCodingNever:
+        return False
+    return choice == HuffmanCodingAlways or enc_len < raw_len

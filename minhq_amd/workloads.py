@@ -1,0 +1,136 @@
+"""Synthetic literal batches for BASELINE.json's configs.
+
+Deterministic and language-neutral: splitmix64 streams, one for literal
+lengths (seed) and one for literal bytes (seed ^ 0xB7E151628AED2A6A).
+
+Byte distributions:
+  hdr   -- byte frequencies of the netbsd.qif header set (errors.log:7-241,
+           217 fields / 5,736 bytes / 61 distinct bytes), add-one smoothed over
+           0x20..0x7E; ~5.8 bits per byte under the RFC 7541 code.
+  print -- uniform over 0x20..0x7E (7.81 bits per byte).
+  adv   -- uniform over the 66 bytes whose code is >= 26 bits (27.35 bits/byte).
+Length distributions:
+  uniform(a, b) -- U{a..b};  zipf -- P(L=k) proportional to 1/(k-3), k in 4..256.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Tuple
+
+import numpy as np
+
+# netbsd.qif byte counts for 0x20..0x7E (errors.log:7-241; see
+# tests/golden/netbsd_qif.json and tests/test_workloads.py which recomputes it).
+NETBSD_HIST = [
+    163, 0, 0, 0, 0, 0, 0, 0, 18, 18, 36, 1, 41, 162, 181, 165, 183, 74, 19, 0, 36, 72, 36, 0, 37, 1,
+    107, 75, 0, 22, 0, 0, 0, 0, 2, 1, 1, 18, 19, 36, 0, 0, 0, 0, 0, 19, 19, 0, 2, 0, 0, 21, 37, 19,
+    0, 36, 0, 1, 0, 0, 0, 0, 0, 4, 0, 331, 45, 343, 115, 540, 57, 180, 163, 198, 4, 41, 135, 78, 326,
+    301, 187, 22, 211, 130, 324, 61, 38, 125, 41, 22, 36, 0, 0, 0, 0,
+]
+
+SEED_NORTH_STAR = 0x6D696E6871  # "minhq"
+SEED_ZIPF = 0x7A697066          # "zipf"
+SEED_ADV = 0x616476             # "adv"
+_BYTE_STREAM_XOR = 0xB7E151628AED2A6A
+
+_GAMMA = np.uint64(0x9E3779B97F4A7C15)
+_M1 = np.uint64(0xBF58476D1CE4E5B9)
+_M2 = np.uint64(0x94D049BB133111EB)
+
+
+def splitmix64(seed: int, count: int, start: int = 0) -> np.ndarray:
+    """Values start..start+count-1 of the splitmix64 sequence seeded by `seed`."""
+    with np.errstate(over="ignore"):
+        idx = np.arange(start + 1, start + count + 1, dtype=np.uint64)
+        z = np.uint64(seed & 0xFFFFFFFFFFFFFFFF) + idx * _GAMMA
+        z = (z ^ (z >> np.uint64(30))) * _M1
+        z = (z ^ (z >> np.uint64(27))) * _M2
+        return z ^ (z >> np.uint64(31))
+
+
+def _unit(r: np.ndarray) -> np.ndarray:
+    return (r >> np.uint64(11)).astype(np.float64) * (1.0 / (1 << 53))
+
+
+def byte_alphabet(dist: str) -> Tuple[np.ndarray, np.ndarray]:
+    """(symbols u8[], cumulative probabilities f64[]) for a byte distribution."""
+    if dist == "hdr":
+        syms = np.arange(0x20, 0x7F, dtype=np.uint8)
+        w = np.asarray(NETBSD_HIST, dtype=np.float64) + 1.0
+    elif dist == "print":
+        syms = np.arange(0x20, 0x7F, dtype=np.uint8)
+        w = np.ones(len(syms))
+    elif dist == "adv":
+        from .hc import code_table  # the kernels' own table (hc/huffmantable.go)
+
+        lens, _ = code_table()
+        syms = np.asarray([s for s in range(256) if lens[s] >= 26], dtype=np.uint8)
+        w = np.ones(len(syms))
+    else:
+        raise ValueError(dist)
+    cdf = np.cumsum(w / w.sum())
+    cdf[-1] = 1.0
+    return syms, cdf
+
+
+def lengths(kind: str, n: int, seed: int, lo: int = 8, hi: int = 56) -> np.ndarray:
+    r = splitmix64(seed, n)
+    if kind == "uniform":
+        span = np.uint64(hi - lo + 1)
+        return (np.uint64(lo) + r % span).astype(np.int64)
+    if kind == "fixed":
+        return np.full(n, lo, dtype=np.int64)
+    if kind == "zipf":  # P(L=k) ~ 1/(k-3), k in 4..256
+        ks = np.arange(4, 257)
+        cdf = np.cumsum(1.0 / (ks - 3))
+        cdf /= cdf[-1]
+        return ks[np.searchsorted(cdf, _unit(r), side="right").clip(0, len(ks) - 1)].astype(np.int64)
+    raise ValueError(kind)
+
+
+@dataclass
+class Batch:
+    data: np.ndarray  # u8, literals back to back
+    off: np.ndarray   # u64, n+1
+    name: str
+
+    @property
+    def n(self) -> int:
+        return len(self.off) - 1
+
+    @property
+    def nbytes(self) -> int:
+        return int(self.off[-1] - self.off[0])
+
+
+def make_batch(n: int, length_kind: str = "uniform", dist: str = "hdr", seed: int = SEED_NORTH_STAR,
+               lo: int = 8, hi: int = 56, name: str = "") -> Batch:
+    L = lengths(length_kind, n, seed, lo, hi)
+    off = np.zeros(n + 1, dtype=np.uint64)
+    off[1:] = np.cumsum(L, dtype=np.uint64)
+    total = int(off[-1])
+    syms, cdf = byte_alphabet(dist)
+    data = np.empty(total, dtype=np.uint8)
+    chunk = 1 << 24
+    for a in range(0, total, chunk):
+        b = min(total, a + chunk)
+        u = _unit(splitmix64(seed ^ _BYTE_STREAM_XOR, b - a, start=a))
+        data[a:b] = syms[np.searchsorted(cdf, u, side="right").clip(0, len(syms) - 1)]
+    return Batch(data, off, name or f"{n}x{length_kind}[{lo},{hi}]/{dist}")
+
+
+# BASELINE.json configs as concrete batches.
+def north_star(n: int = 1 << 20) -> Batch:
+    return make_batch(n, "uniform", "hdr", SEED_NORTH_STAR, 8, 56, "northstar-1Mx U{8..56} hdr")
+
+
+def config2(n: int = 1 << 20, dist: str = "hdr") -> Batch:
+    return make_batch(n, "uniform", dist, SEED_NORTH_STAR, 8, 64, f"config2-1Mx U{{8..64}} {dist}")
+
+
+def config4(n: int = 1 << 24) -> Batch:
+    return make_batch(n, "zipf", "hdr", SEED_ZIPF, name="config4-16Mx zipf{4..256} hdr")
+
+
+def config5(n: int = 4 << 20) -> Batch:
+    return make_batch(n, "fixed", "adv", SEED_ADV, 128, 128, "config5-4Mx128B adv")

@@ -1,0 +1,235 @@
+"""GPU parity: the HIP kernels (through the C ABI) vs the CPU oracle and the
+reference's golden vectors.  Bit-exact throughout (integer/byte work).
+
+Sizes: golden vectors and edge cases; random literals; every BASELINE.json
+config at a size the oracle finishes in seconds; and full-size properties
+(encode -> decode round trip, out_len == plaintext length) at config sizes.
+"""
+import random
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def codec():
+    from minhq_amd import build, hc
+
+    build.build()
+    c = hc.Codec(1)
+    yield c
+    c.close()
+
+
+def _oracle_encode_batch(oracle_mod, data, off):
+    enc_len = oracle_mod.encode_len_batch(data, off, nthreads=8)
+    eoff = np.zeros(len(off), dtype=np.uint64)
+    eoff[1:] = np.cumsum(enc_len, dtype=np.uint64)
+    return enc_len, oracle_mod.encode_batch(data, off, eoff, nthreads=8), eoff
+
+
+def _check_batch(codec, oracle_mod, data, off):
+    """Encode+decode a packed batch on the GPU; compare with the oracle."""
+    from minhq_amd import hc
+
+    enc_len_ref, enc_ref, eoff = _oracle_encode_batch(oracle_mod, data, off)
+    assert np.array_equal(codec.encode_len(data, off), enc_len_ref)
+    enc, eoff_gpu = codec.encode(data, off)
+    assert np.array_equal(eoff_gpu, eoff)
+    assert enc.tobytes() == enc_ref.tobytes()
+    cap = hc.capacity_offsets(eoff)
+    out_ref, len_ref, st_ref = oracle_mod.decode_batch(enc_ref, eoff, cap, nthreads=8)
+    out, cap2, out_len, status = codec.decode(enc_ref, eoff, cap)
+    assert np.array_equal(out_len, len_ref)
+    assert np.array_equal(status, st_ref)
+    # compare only the defined bytes of each region
+    mask = np.zeros(len(out_ref), dtype=bool)
+    starts = cap[:-1].astype(np.int64)
+    lens = len_ref.astype(np.int64)
+    idx = np.repeat(starts, lens) + (np.arange(lens.sum()) - np.repeat(np.cumsum(lens) - lens, lens))
+    mask[idx] = True
+    assert np.array_equal(out[: len(out_ref)][mask], out_ref[mask])
+    # and the decode reproduces the plaintext
+    assert np.array_equal(out_len.astype(np.uint64), np.diff(off))
+    assert np.array_equal(out[: len(out_ref)][mask], data)
+
+
+def test_golden_vectors_batch(codec, golden):
+    from minhq_amd import hc
+
+    vecs = golden("huffman_vectors.json") + golden("embedded_literals.json")
+    texts = [v["text"].encode() for v in vecs]
+    encs = [bytes.fromhex(v["hex"]) for v in vecs]
+    assert hc.HuffmanEncodeBatch(texts, codec) == encs
+    vals, errs = hc.HuffmanDecodeBatch(encs, codec)
+    assert vals == texts and errs == [None] * len(vecs)
+
+
+EDGE = [
+    ("", b"", 0), ("ff", b"", 0), ("ffff", b"", 0), ("00", b"0", 0), ("07", b"0", 0),
+    ("3fffffff", b"o", 0), ("fffffffc", b"", 1), ("fffffffd", b"", 1), ("ffffffff", b"", 1),
+    ("ffffffffff", b"", 1),
+]
+
+
+def test_edge_cases(codec, oracle_mod):
+    from minhq_amd import hc
+
+    encs = [bytes.fromhex(h) for h, _, _ in EDGE]
+    # add 30-ones-at-end (accepted) and 31st-bit (invalid) cases, and an invalid tail after text
+    encs.append(int("00011" + "00011" + "1" * 30, 2).to_bytes(5, "big"))
+    encs.append(int("00011" + "1" * 30 + "0" * 5, 2).to_bytes(5, "big"))
+    encs.append(oracle_mod.encode(b"abc") + bytes.fromhex("ffffffff"))
+    vals, errs = hc.HuffmanDecodeBatch(encs, codec)
+    for e, v, err in zip(encs, vals, errs):
+        ref, st = oracle_mod.decode(e)
+        assert v == ref, e.hex()
+        assert (err is not None) == (st == 1), e.hex()
+    assert [v for v in vals[: len(EDGE)]] == [t for _, t, _ in EDGE]
+
+
+def test_every_symbol_and_long_codes(codec, oracle_mod):
+    from minhq_amd import hc
+
+    lits = [bytes(range(256)), bytes(range(255, -1, -1)), bytes([0] * 64), bytes([255] * 64),
+            bytes([10, 13, 22] * 40), b"0" * 1000, bytes(range(128, 256)) * 9]
+    enc = hc.HuffmanEncodeBatch(lits, codec)
+    assert enc == [oracle_mod.encode(x) for x in lits]
+    vals, errs = hc.HuffmanDecodeBatch(enc, codec)
+    assert vals == lits and errs == [None] * len(lits)
+
+
+def test_random_bytes_round_trip(codec, oracle_mod):
+    rng = random.Random(99)
+    lits = [bytes(rng.randrange(256) for _ in range(rng.randrange(0, 90))) for _ in range(5000)]
+    from minhq_amd import hc
+
+    data, off = hc.pack(lits)
+    _check_batch(codec, oracle_mod, data, off)
+
+
+def test_random_garbage_decode(codec, oracle_mod):
+    """Arbitrary bytes as encoded input: exercises INVALID, partial codes and truncation."""
+    from minhq_amd import hc
+
+    rng = np.random.default_rng(5)
+    lens = rng.integers(0, 48, size=20000)
+    off = np.zeros(len(lens) + 1, dtype=np.uint64)
+    off[1:] = np.cumsum(lens)
+    # bias toward 0xff so the EOS prefix appears often
+    data = np.where(rng.random(int(off[-1])) < 0.5, 0xFF, rng.integers(0, 256, int(off[-1]))).astype(np.uint8)
+    cap = hc.capacity_offsets(off)
+    out_ref, len_ref, st_ref = oracle_mod.decode_batch(data, off, cap, nthreads=8)
+    out, _, out_len, status = codec.decode(data, off, cap)
+    assert np.array_equal(out_len, len_ref)
+    assert np.array_equal(status, st_ref)
+    assert st_ref.sum() > 100  # the INVALID path really is exercised
+    for i in range(len(lens)):
+        a = int(cap[i])
+        assert out[a: a + int(len_ref[i])].tobytes() == out_ref[a: a + int(len_ref[i])].tobytes()
+
+
+def test_truncating_capacity(codec, oracle_mod):
+    """A region smaller than the decoded length is filled and the literal stops OK
+    (Read returns once p is full, hc/huffman.go:104)."""
+    from minhq_amd import hc
+
+    lits = [b"www.example.com", b"0" * 40, b"custom-value"]
+    enc = [oracle_mod.encode(x) for x in lits]
+    data, off = hc.pack(enc)
+    cap = np.array([0, 4, 4 + 7, 4 + 7 + 100], dtype=np.uint64)
+    out, _, out_len, status = codec.decode(data, off, cap)
+    for i, e in enumerate(enc):
+        c = int(cap[i + 1] - cap[i])
+        ref, st = oracle_mod.decode(e, cap=c)
+        assert out[int(cap[i]): int(cap[i]) + int(out_len[i])].tobytes() == ref
+        assert status[i] == st
+
+
+@pytest.mark.parametrize("dist", ["hdr", "print", "adv"])
+def test_config_batches_vs_oracle(codec, oracle_mod, dist):
+    from minhq_amd import workloads
+
+    lo, hi = (128, 128) if dist == "adv" else (8, 64)
+    b = workloads.make_batch(20000, "fixed" if dist == "adv" else "uniform", dist, lo=lo, hi=hi)
+    _check_batch(codec, oracle_mod, b.data, b.off)
+
+
+def test_zipf_batch_vs_oracle(codec, oracle_mod):
+    from minhq_amd import workloads
+
+    b = workloads.make_batch(30000, "zipf", "hdr", workloads.SEED_ZIPF)
+    _check_batch(codec, oracle_mod, b.data, b.off)
+
+
+def test_qif_corpus_literals(codec, oracle_mod, golden):
+    """Config 3: every literal of the netbsd.qif header set (errors.log:7-241) plus
+    the reference test-case texts, tiled to 2^16 literals, bit-exact vs the oracle."""
+    from minhq_amd import hc
+
+    lits = []
+    for f in golden("netbsd_qif.json")["fields"]:
+        if f:
+            lits += [f[0].encode(), f[1].encode()]
+    lits += [r["text"].encode() for r in golden("embedded_literals.json")]
+    tiled = (lits * (65536 // len(lits) + 1))[:65536]
+    data, off = hc.pack(tiled)
+    _check_batch(codec, oracle_mod, data, off)
+
+
+def test_unaligned_offsets_and_bias(codec, oracle_mod):
+    """Host entry points accept offsets that do not start at 0."""
+    from minhq_amd import hc
+
+    lits = [b"abc", b"gzip", b"", b"x" * 33]
+    enc = [oracle_mod.encode(x) for x in lits]
+    data, off = hc.pack(enc)
+    off = off + np.uint64(1000)
+    cap = hc.capacity_offsets(off) + np.uint64(77)
+    out, _, out_len, status = codec.decode(data, off, cap)
+    for i, x in enumerate(lits):
+        a = int(cap[i] - cap[0])
+        assert out[a: a + int(out_len[i])].tobytes() == x
+
+
+def test_device_resident_round_trip_full_size(codec):
+    """Config 2 at full size (2^20 literals) through the device entry points:
+    encode -> offsets -> decode reproduces the plaintext exactly."""
+    import torch
+
+    from minhq_amd import workloads
+
+    b = workloads.config2()
+    dev = torch.device("cuda:0")
+    data = torch.from_numpy(b.data).to(dev)
+    off = torch.from_numpy(b.off.view(np.int64)).to(dev)
+    n = b.n
+    enc_len = torch.empty(n, dtype=torch.int32, device=dev)
+    enc_off = torch.empty(n + 1, dtype=torch.int64, device=dev)
+    cap_off = torch.empty(n + 1, dtype=torch.int64, device=dev)
+    codec.encode_len_dev(data, off, enc_len)
+    codec.offsets_dev(enc_len, enc_off, cap_off)
+    total = int(enc_off[-1].item())
+    enc = torch.empty(max(total, 1), dtype=torch.uint8, device=dev)
+    codec.encode_dev(data, off, enc, enc_off)
+    out = torch.empty(int(cap_off[-1].item()) + 1, dtype=torch.uint8, device=dev)
+    out_len = torch.empty(n, dtype=torch.int32, device=dev)
+    status = torch.empty(n, dtype=torch.uint8, device=dev)
+    codec.decode_dev(enc, enc_off, out, cap_off, out_len, status)
+    torch.cuda.synchronize()
+    assert int(status.sum().item()) == 0
+    assert torch.equal(out_len.long(), (off[1:] - off[:-1]))
+    # gather decoded bytes and compare with the plaintext
+    cap = cap_off[:-1]
+    lens = out_len.long()
+    rep = torch.repeat_interleave(cap, lens)
+    within = torch.arange(int(lens.sum().item()), device=dev) - torch.repeat_interleave(
+        torch.cumsum(lens, 0) - lens, lens)
+    assert torch.equal(out[rep + within], data)
+    # capacity_dev on the encoded offsets equals the offsets pass's capacities
+    cap2 = torch.empty_like(cap_off)
+    codec.capacity_dev(enc_off, cap2)
+    torch.cuda.synchronize()
+    assert torch.equal(cap2, cap_off)
