@@ -64,6 +64,16 @@ def load():
     """Loads the in-tree libmhq_huff.so (raises OSError if it is absent)."""
     global _lib
     if _lib is None:
+        # One HIP runtime per process: PyTorch wheels bundle their own
+        # libamdhip64 (SONAME libamdhip64.so.7).  Importing torch first makes
+        # the dynamic linker bind this library to that same runtime, so torch
+        # streams, events and allocations are valid handles here.  Loaded the
+        # other way round, torch would bring up a second runtime that finds no
+        # GPU.  Without torch (a Go/cgo host) /opt/rocm's runtime is used.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         if not os.path.exists(LIB_PATH):
             raise OSError(f"{LIB_PATH} is missing: run `python -m minhq_amd.build` "
                           "(or __graft_entry__.build()) first")
