@@ -2,15 +2,24 @@
 // batch codec.  Bit-exact with minhq's hc/huffman.go + io/bitio.go (semantics
 // contract: SURVEY.md §8a; restated in oracle/huff_oracle.c).
 //
-// Work decomposition (decode, encode, encode_len alike):
-//   * a workgroup is 4 wave64s; each wave owns a tile of kLitsPerWave
-//     consecutive literals;
-//   * the wave stages the tile's offsets in LDS and splits the tile into 64
-//     contiguous literal runs of near-equal encoded bytes (a lower_bound per
-//     lane), so every lane streams one contiguous byte range in and one out;
-//   * the code tables live in LDS: LUT1 (4096 x u32, two symbols per probe)
-//     and LUT2 (leading-ones keyed, codes of 13..30 bits) for decode, the 256
-//     code/length pairs for encode.
+// Work decomposition (all three codec kernels):
+//   * a workgroup is kWaves wave64s sharing the code tables in LDS; every wave
+//     independently walks tiles of kTileLits consecutive literals;
+//   * a tile is staged through LDS: its offsets (coalesced u64 loads), its
+//     input bytes (coalesced 16-B loads; decode input is stored byte-swapped
+//     so bit 31 of a word is the first stream bit), and for decode/encode the
+//     whole output region, zero-filled, in global layout, written back with
+//     aligned 16-B stores;
+//   * if a tile does not fit the wave's LDS slice it is processed as several
+//     sub-tiles (maximal prefixes that fit); a single literal too large for
+//     the slice is handled by one lane straight from global memory;
+//   * inside a (sub-)tile each lane owns a contiguous run of literals holding
+//     ~1/64 of the tile's input bytes (lower_bound per lane) and streams it
+//     with one flat loop: literal boundaries are a branch inside the loop, not
+//     a loop nest, so lanes never wait for each other's literals.
+//
+// Decode probes LUT1 (4096 x u32, up to two symbols per 12-bit probe) and, for
+// codes of 13..30 bits, LUT2 keyed by the count of leading ones (huff_table.h).
 #include <hip/hip_runtime.h>
 
 #include "huff_kernels.h"
@@ -21,260 +30,531 @@ namespace mhq {
 namespace {
 
 constexpr int kWave = 64;
-constexpr int kWavesPerBlock = 4;
-constexpr int kBlock = kWave * kWavesPerBlock;
-constexpr int kLitsPerWave = 512;
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
-// ---------------------------------------------------------------------------
-// Tile setup shared by all three kernels.
-// ---------------------------------------------------------------------------
-struct TileRun {
-  uint32_t first, last;  // this lane's literal run [first, last) within the tile
-  uint32_t cnt;          // literals in the tile
-  uint64_t s;            // tile's first literal
-};
-
-// Loads off[s .. s+cnt] into `lds` (cnt+1 entries).  Caller synchronises.
-__device__ inline void load_tile_offsets(const uint64_t *__restrict__ off, uint64_t s, uint32_t cnt,
-                                         uint64_t *lds, int lane) {
-  for (uint32_t j = lane; j <= cnt; j += kWave) lds[j] = off[s + j];
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// First index j in [0, cnt) with lds[j] >= target, or cnt.
-__device__ inline uint32_t lower_bound_lds(const uint64_t *lds, uint32_t cnt, uint64_t target) {
-  uint32_t lo = 0, hi = cnt;
+__device__ __forceinline__ uint32_t popc64(uint64_t m) { return (uint32_t)__popcll(m); }
+
+// ---------------------------------------------------------------------------
+// Tile plumbing shared by the kernels.
+// ---------------------------------------------------------------------------
+template <int kTileLits>
+struct TileOffsets {
+  static constexpr int kPer = (kTileLits + 1 + kWave - 1) / kWave;
+  uint64_t io[kPer];  // in_off[s + lane + 64k]
+  uint64_t oo[kPer];  // out_off[s + lane + 64k] (unused by encode_len)
+
+  __device__ __forceinline__ void load(const uint64_t *__restrict__ in_off, const uint64_t *__restrict__ out_off,
+                                       uint64_t s, uint32_t cnt, int lane) {
+#pragma unroll
+    for (int k = 0; k < kPer; k++) {
+      const uint32_t j = (uint32_t)lane + (uint32_t)k * kWave;
+      io[k] = j <= cnt ? __builtin_nontemporal_load(in_off + s + j) : 0;
+      oo[k] = (out_off && j <= cnt) ? __builtin_nontemporal_load(out_off + s + j) : 0;
+    }
+  }
+
+  // Literals [cur, end] fit when their input span (from the 16-B aligned start)
+  // is <= in_lim and their output span <= out_lim.  Returns end (>= cur; == cur
+  // means literal `cur` alone does not fit).
+  __device__ __forceinline__ uint32_t fit(uint32_t cur, uint32_t cnt, uint64_t in_lo, uint64_t in_lim,
+                                          uint64_t out_lo, uint64_t out_lim, int lane) const {
+    uint32_t n = 0;
+#pragma unroll
+    for (int k = 0; k < kPer; k++) {
+      const uint32_t j = (uint32_t)lane + (uint32_t)k * kWave;
+      const bool ok = j > cur && j <= cnt && (io[k] - in_lo) <= in_lim && (oo[k] - out_lo) <= out_lim;
+      n += popc64(__ballot(ok));
+    }
+    return cur + n;
+  }
+};
+
+// First index i in [0, m) with key(i) >= target, or m.
+template <class K>
+__device__ __forceinline__ uint32_t lower_bound(K key, uint32_t m, uint32_t target) {
+  uint32_t lo = 0, hi = m;
   while (lo < hi) {
-    uint32_t mid = (lo + hi) >> 1;
-    if (lds[mid] < target) lo = mid + 1;
+    const uint32_t mid = (lo + hi) >> 1;
+    if (key(mid) < target) lo = mid + 1;
     else hi = mid;
   }
   return lo;
 }
 
-// Byte-balanced split of the tile into 64 contiguous literal runs.
-__device__ inline void split_runs(const uint64_t *lds_in, uint32_t cnt, int lane, TileRun &r) {
-  const uint64_t b0 = lds_in[0];
-  const uint64_t total = lds_in[cnt] - b0;
-  const uint64_t t0 = b0 + (total * (uint64_t)lane) / kWave;
-  const uint64_t t1 = b0 + (total * (uint64_t)(lane + 1)) / kWave;
-  r.first = lane == 0 ? 0u : lower_bound_lds(lds_in, cnt, t0);
-  r.last = lane == kWave - 1 ? cnt : lower_bound_lds(lds_in, cnt, t1);
+// Byte-balanced split of literals [0, m) (input byte starts key(i)) into 64
+// contiguous runs.
+template <class K>
+__device__ __forceinline__ void lane_run(K key, uint32_t m, int lane, uint32_t &first, uint32_t &last) {
+  const uint32_t b0 = key(0);
+  const uint32_t total = key(m) - b0;
+  const uint32_t t0 = b0 + (uint32_t)(((uint64_t)total * (uint32_t)lane) >> 6);
+  const uint32_t t1 = b0 + (uint32_t)(((uint64_t)total * (uint32_t)(lane + 1)) >> 6);
+  first = lane == 0 ? 0u : lower_bound(key, m, t0);
+  last = lane == kWave - 1 ? m : lower_bound(key, m, t1);
+}
+
+// Copies global bytes [a, a+nbytes) (a 16-B aligned address) into LDS words.
+template <bool kSwap>
+__device__ __forceinline__ void stage_in(uint32_t *lds, const uint8_t *a, uint32_t nbytes, int lane) {
+  const uint32_t chunks = (nbytes + 15u) >> 4;
+  const u32x4 *src = (const u32x4 *)a;
+  for (uint32_t c = lane; c < chunks; c += kWave) {
+    u32x4 v = __builtin_nontemporal_load(src + c);  // an aligned chunk holding a valid byte never crosses a page
+    if (kSwap) {
+      v.x = __builtin_bswap32(v.x);
+      v.y = __builtin_bswap32(v.y);
+      v.z = __builtin_bswap32(v.z);
+      v.w = __builtin_bswap32(v.w);
+    }
+    *(u32x4 *)(lds + 4 * c) = v;
+  }
+}
+
+__device__ __forceinline__ void zero_lds(uint8_t *lds, uint32_t nbytes, int lane) {
+  const uint32_t chunks = (nbytes + 15u) >> 4;
+  for (uint32_t c = lane; c < chunks; c += kWave) *(uint4 *)(lds + 16 * c) = make_uint4(0, 0, 0, 0);
+}
+
+// Writes LDS bytes [lo, hi) to global o_al + [lo, hi), o_al 16-B aligned.
+// Whole 16-B chunks go out as one aligned store; the (at most two) partial
+// chunks at the ends are written byte by byte so neighbours are untouched.
+__device__ __forceinline__ void store_out(uint8_t *o_al, const uint8_t *lds, uint32_t lo, uint32_t hi, int lane) {
+  if (hi <= lo) return;
+  const uint32_t c0 = lo >> 4, c1 = (hi + 15u) >> 4;
+  for (uint32_t c = c0 + lane; c < c1; c += kWave) {
+    const uint32_t a = c << 4, b = a + 16u;
+    if (a >= lo && b <= hi) {
+      __builtin_nontemporal_store(*(const u32x4 *)(lds + a), (u32x4 *)(o_al + a));
+    } else {
+      const uint32_t x0 = a > lo ? a : lo, x1 = b < hi ? b : hi;
+      for (uint32_t x = x0; x < x1; x++) o_al[x] = lds[x];
+    }
+  }
 }
 
 // ---------------------------------------------------------------------------
-// Word-granular reader over a tile's input bytes.  Words are fetched aligned
-// and byte-swapped so bit 31 is the first bit of the stream (MSB-first, as
-// io/bitio.go:202-214 reads it).  Fetches past the tile's last byte are
-// clamped to the last in-range word: those bits are never used for a decision
-// (see decode_lane).
+// Decode (hc/huffman.go:102-121 + the ReadFull loop, hc/io.go:85-96).
 // ---------------------------------------------------------------------------
-struct WordReader {
-  const uint32_t *base;  // 4-byte aligned
-  uint64_t lastw;        // index of the last word holding a tile byte
-  __device__ inline uint32_t word(uint64_t k) const {
-    k = k < lastw ? k : lastw;
-    return __builtin_bswap32(__builtin_nontemporal_load(base + k));
-  }
-  // 32 stream bits starting at bit position bp.
-  __device__ inline uint32_t window(uint64_t bp) const {
-    const uint64_t k = bp >> 5;
-    const uint32_t sh = (uint32_t)bp & 31u;
-    const uint32_t a = word(k);
-    const uint32_t b = word(k + 1);
-    return sh ? (a << sh) | (b >> (32u - sh)) : a;
-  }
+namespace dec {
+constexpr int kWaves = 8;
+constexpr int kThreads = kWave * kWaves;
+constexpr int kTileLits = 256;
+constexpr int kInCap = 6144;   // staged input bytes per wave (incl. 16-B alignment slack)
+constexpr int kOutCap = 8192;  // staged output bytes per wave
+
+struct WaveSmem {
+  uint32_t in_w[kInCap / 4 + 4];  // byte-swapped input words (+ tail for window reads)
+  uint8_t out_b[kOutCap + kWave]; // output staging (+ one junk byte per lane)
+  uint2 rec[kTileLits + 1];       // per boundary: (input byte index, output byte index)
+  uint32_t olen[kTileLits];       // out_len | status << 31
 };
-
-__device__ inline WordReader make_reader(const uint8_t *in, uint64_t start, uint64_t end) {
-  WordReader r;
-  const uintptr_t a0 = (uintptr_t)(in + start) & ~(uintptr_t)3;
-  r.base = (const uint32_t *)a0;
-  const uintptr_t last_byte = (uintptr_t)(in + (end > start ? end - 1 : start));
-  r.lastw = (uint64_t)((last_byte - a0) >> 2);
-  return r;
-}
-
-// ---------------------------------------------------------------------------
-// Decode: hc/huffman.go:102-121 (+ ReadFull loop semantics, hc/io.go:92-96).
-// ---------------------------------------------------------------------------
-struct DecodeSmem {
+struct Smem {
   uint32_t lut1[kLut1Size];
   uint16_t lut2[kLut2Size];
-  uint64_t in_off[kWavesPerBlock][kLitsPerWave + 1];
-  uint64_t out_off[kWavesPerBlock][kLitsPerWave + 1];
+  WaveSmem w[kWaves];
 };
+}  // namespace dec
 
-__global__ __launch_bounds__(kBlock) void decode_kernel(
+// One literal, one lane, straight from global memory: literals too large for a
+// wave's LDS slice.  Same decision rules as the staged loop.
+__device__ void decode_literal_global(const uint8_t *src, uint64_t nbytes, uint8_t *dst, uint64_t cap,
+                                      const uint32_t *lut1, const uint16_t *lut2, uint32_t *out_len,
+                                      uint8_t *status) {
+  const uintptr_t a0 = (uintptr_t)src & ~(uintptr_t)3;
+  const uint32_t *wb = (const uint32_t *)a0;
+  const uint64_t bit0 = ((uintptr_t)src & 3u) * 8u;
+  const uint64_t endbit = bit0 + nbytes * 8u;
+  const uint64_t lastw = nbytes ? ((uintptr_t)(src + nbytes - 1) - a0) >> 2 : 0;
+  uint64_t p = bit0, n = 0;
+  uint8_t st = 0;
+  while (n < cap && p < endbit) {
+    const uint64_t rem = endbit - p;
+    const uint64_t k = p >> 5;
+    const uint32_t s = (uint32_t)p & 31u;
+    const uint32_t w0 = __builtin_bswap32(wb[k < lastw ? k : lastw]);
+    const uint32_t w1 = __builtin_bswap32(wb[k + 1 < lastw ? k + 1 : lastw]);
+    const uint32_t win = s ? (w0 << s) | (w1 >> (32u - s)) : w0;
+    const uint32_t e = lut1[win >> (32 - kLut1Bits)];
+    const uint32_t nsym = e >> 26;
+    if (nsym == 0) {
+      const uint32_t nw = ~win;
+      const uint32_t c = nw ? (uint32_t)__builtin_clz(nw) : 32u;
+      if (c >= (uint32_t)kEosOnes) {
+        st = rem > (uint64_t)kEosOnes;
+        break;
+      }
+      const uint32_t e2 = lut2[(c << kLut2SubBits) | ((win << (c + 1)) >> (32 - kLut2SubBits))];
+      const uint32_t L = e2 >> 8;
+      if (L == 0 || L > rem) break;
+      dst[n++] = (uint8_t)e2;
+      p += L;
+      continue;
+    }
+    const uint32_t len0 = (e >> 16) & 31u, tot = (e >> 21) & 31u;
+    if (len0 > rem) break;
+    dst[n++] = (uint8_t)e;
+    if (nsym == 2 && tot <= rem && n < cap) {
+      dst[n++] = (uint8_t)(e >> 8);
+      p += tot;
+    } else {
+      p += len0;
+    }
+  }
+  *out_len = (uint32_t)n;
+  *status = st;
+}
+
+__global__ __launch_bounds__(dec::kThreads) void decode_kernel(
     const uint8_t *__restrict__ in, const uint64_t *__restrict__ in_off, uint64_t in_bias, uint64_t n,
     uint8_t *__restrict__ out, const uint64_t *__restrict__ out_off, uint64_t out_bias,
     uint32_t *__restrict__ out_len, uint8_t *__restrict__ status, const uint32_t *__restrict__ g_lut1,
-    const uint16_t *__restrict__ g_lut2) {
-  __shared__ DecodeSmem sm;
+    const uint16_t *__restrict__ g_lut2, uint64_t ntiles) {
+  using namespace dec;
+  __shared__ Smem sm;
   const int tid = threadIdx.x;
-  const int wave = tid / kWave;
+  const int wave = __builtin_amdgcn_readfirstlane(tid / kWave);
   const int lane = tid % kWave;
-
-  for (int i = tid; i < kLut1Size; i += kBlock) sm.lut1[i] = g_lut1[i];
-  for (int i = tid; i < kLut2Size; i += kBlock) sm.lut2[i] = g_lut2[i];
-
-  const uint64_t s = ((uint64_t)blockIdx.x * kWavesPerBlock + wave) * kLitsPerWave;
-  const uint32_t cnt = s < n ? (uint32_t)min((uint64_t)kLitsPerWave, n - s) : 0u;
-  if (cnt) {
-    load_tile_offsets(in_off, s, cnt, sm.in_off[wave], lane);
-    load_tile_offsets(out_off, s, cnt, sm.out_off[wave], lane);
-  }
+  for (int i = tid; i < kLut1Size / 4; i += kThreads) ((uint4 *)sm.lut1)[i] = ((const uint4 *)g_lut1)[i];
+  for (int i = tid; i < kLut2Size / 8; i += kThreads) ((uint4 *)sm.lut2)[i] = ((const uint4 *)g_lut2)[i];
   __syncthreads();
-  if (!cnt) return;
 
-  const uint64_t *lin = sm.in_off[wave];
-  const uint64_t *lout = sm.out_off[wave];
-  TileRun run;
-  split_runs(lin, cnt, lane, run);
+  WaveSmem &ws = sm.w[wave];
+  const uint32_t *lut1 = sm.lut1;
+  const uint16_t *lut2 = sm.lut2;
+  const uint64_t stride = (uint64_t)gridDim.x * kWaves;
 
-  const uint64_t tile_start = lin[0] - in_bias;
-  const uint64_t tile_end = lin[cnt] - in_bias;
-  const WordReader rd = make_reader(in, tile_start, tile_end);
-  const uint64_t bit0 = ((uintptr_t)(in + tile_start) & 3u) * 8u;  // bit offset of tile start in word 0
+  for (uint64_t t = (uint64_t)blockIdx.x * kWaves + wave; t < ntiles; t += stride) {
+    const uint64_t s = t * kTileLits;
+    const uint32_t cnt = (uint32_t)min((uint64_t)kTileLits, n - s);
+    TileOffsets<kTileLits> off;
+    off.load(in_off, out_off, s, cnt, lane);
 
-  for (uint32_t j = run.first; j < run.last; j++) {
-    uint64_t bp = bit0 + (lin[j] - lin[0]) * 8u;
-    const uint64_t endbit = bit0 + (lin[j + 1] - lin[0]) * 8u;
-    uint8_t *dst = out + (lout[j] - out_bias);
-    const uint64_t cap = lout[j + 1] - lout[j];
-    uint64_t cnt_out = 0;
-    uint8_t st = 0;
-    while (cnt_out < cap) {
-      const uint64_t rem = endbit - bp;
-      if (rem == 0) break;  // io.EOF at a symbol boundary
-      const uint32_t w = rd.window(bp);
-      const uint32_t e = sm.lut1[w >> (32 - kLut1Bits)];
-      const uint32_t nsym = e >> 26;
-      if (nsym == 0) {
-        // Long code (> 12 bits) or the all-ones EOS prefix.
-        const uint32_t nw = ~w;
-        const uint32_t c = nw ? (uint32_t)__builtin_clz(nw) : 32u;  // leading ones
-        if (c >= (uint32_t)kEosOnes) {
-          // 30 ones reach the childless node (hc/huffman.go:63-76): one more
-          // bit is a nil child -> "invalid Huffman coding"; otherwise EOF.
-          if (rem > (uint64_t)kEosOnes) st = 1;
-          break;
-        }
-        const uint32_t sub = (w << (c + 1)) >> (32 - kLut2SubBits);
-        const uint32_t e2 = sm.lut2[(c << kLut2SubBits) | sub];
-        const uint32_t L = e2 >> 8;
-        if (L == 0 || L > rem) break;  // partial code at the end: dropped
-        dst[cnt_out++] = (uint8_t)(e2 & 0xffu);
-        bp += L;
+    uint32_t cur = 0;
+    while (cur < cnt) {
+      const uint64_t ic = in_off[s + cur], oc = out_off[s + cur];  // wave-uniform (scalar loads)
+      const uint8_t *ia = in + (ic - in_bias);
+      uint8_t *oa = out + (oc - out_bias);
+      const uint32_t idelta = (uint32_t)((uintptr_t)ia & 15u);
+      const uint32_t odelta = (uint32_t)((uintptr_t)oa & 15u);
+      const uint32_t end = off.fit(cur, cnt, ic, kInCap - idelta, oc, kOutCap - odelta, lane);
+      if (end == cur) {  // one literal larger than the slice
+        if (lane == 0)
+          decode_literal_global(ia, in_off[s + cur + 1] - ic, oa, out_off[s + cur + 1] - oc, lut1, lut2,
+                                out_len + s + cur, status + s + cur);
+        cur++;
         continue;
       }
-      const uint32_t len0 = (e >> 16) & 31u;
-      const uint32_t tot = (e >> 21) & 31u;
-      if (len0 > rem) break;  // partial code: dropped silently
-      dst[cnt_out++] = (uint8_t)(e & 0xffu);
-      if (nsym == 2 && tot <= rem && cnt_out < cap) {
-        dst[cnt_out++] = (uint8_t)((e >> 8) & 0xffu);
-        bp += tot;
-      } else {
-        bp += len0;
+      const uint32_t m = end - cur;
+      // boundary records relative to the staged slices
+#pragma unroll
+      for (int k = 0; k < TileOffsets<kTileLits>::kPer; k++) {
+        const uint32_t j = (uint32_t)lane + (uint32_t)k * kWave;
+        if (j >= cur && j <= end)
+          ws.rec[j - cur] = make_uint2((uint32_t)(off.io[k] - ic) + idelta, (uint32_t)(off.oo[k] - oc) + odelta);
       }
+      const uint32_t in_bytes = (uint32_t)(in_off[s + end] - ic) + idelta;
+      const uint32_t out_bytes = (uint32_t)(out_off[s + end] - oc) + odelta;
+      stage_in<true>(ws.in_w, ia - idelta, in_bytes, lane);
+      zero_lds(ws.out_b, out_bytes, lane);
+      wave_sync();
+
+      uint32_t j, last;
+      lane_run([&](uint32_t i) { return ws.rec[i].x; }, m, lane, j, last);
+      if (j < last) {
+        uint32_t p = ws.rec[j].x * 8u;
+        uint2 r = ws.rec[j + 1];
+        uint32_t endbit = r.x * 8u;
+        uint32_t optr = ws.rec[j].y, ostart = optr, oend = r.y;
+        const uint32_t junk = kOutCap + (uint32_t)lane;
+        while (true) {
+          const uint32_t rem = endbit - p;
+          const uint32_t k = p >> 5, sh = p & 31u;
+          const uint32_t w0 = ws.in_w[k], w1 = ws.in_w[k + 1];
+          const uint32_t win = sh ? __builtin_amdgcn_alignbit(w0, w1, 32u - sh) : w0;
+          const uint32_t e = lut1[win >> (32 - kLut1Bits)];
+          uint32_t cnt_s, adv, syms, bad = 0;
+          if (e >> 26) {  // one or two codes of <= 12 bits
+            const uint32_t len0 = (e >> 16) & 31u, tot = (e >> 21) & 31u;
+            const bool both = tot <= rem;
+            cnt_s = both ? (e >> 26) : (len0 <= rem ? 1u : 0u);
+            adv = both ? tot : len0;
+            syms = e;
+          } else {  // a code of 13..30 bits, or the all-ones EOS prefix
+            const uint32_t nw = ~win;
+            const uint32_t c = nw ? (uint32_t)__builtin_clz(nw) : 32u;
+            if (c >= (uint32_t)kEosOnes) {
+              cnt_s = 0;
+              adv = 0;
+              syms = 0;
+              bad = rem > (uint32_t)kEosOnes;  // a 31st bit exists: nil child
+            } else {
+              const uint32_t e2 = lut2[(c << kLut2SubBits) | ((win << (c + 1)) >> (32 - kLut2SubBits))];
+              const uint32_t L = e2 >> 8;
+              cnt_s = (L != 0 && L <= rem) ? 1u : 0u;
+              adv = L;
+              syms = e2 & 0xffu;
+            }
+          }
+          // Read() returns as soon as its buffer is full (hc/huffman.go:104)
+          const uint32_t room = oend - optr;
+          if (room == 0) {
+            cnt_s = 0;
+            bad = 0;
+          } else if (cnt_s > room) {
+            cnt_s = room;
+          }
+          ws.out_b[cnt_s >= 1 ? optr : junk] = (uint8_t)syms;
+          ws.out_b[cnt_s >= 2 ? optr + 1 : junk] = (uint8_t)(syms >> 8);
+          optr += cnt_s;
+          if (cnt_s == 0) {  // end of this literal
+            ws.olen[j] = (optr - ostart) | (bad << 31);
+            if (++j >= last) break;
+            p = endbit;
+            r = ws.rec[j + 1];
+            endbit = r.x * 8u;
+            ostart = optr = oend;
+            oend = r.y;
+          } else {
+            p += adv;
+          }
+        }
+      }
+      wave_sync();
+      store_out(oa - odelta, ws.out_b, odelta, out_bytes, lane);
+      for (uint32_t i = lane; i < m; i += kWave) {
+        const uint32_t v = ws.olen[i];
+        out_len[s + cur + i] = v & 0x7fffffffu;
+        status[s + cur + i] = (uint8_t)(v >> 31);
+      }
+      wave_sync();
+      cur = end;
     }
-    out_len[s + j] = (uint32_t)cnt_out;
-    status[s + j] = st;
   }
 }
 
 // ---------------------------------------------------------------------------
-// Encode length: sum of code lengths per literal -> bytes (hc/huffman.go:23-37
-// + Pad).  This is also the input to the Auto decision (hc/io.go:172).
+// Encode length (hc/huffman.go:23-37 sizing; the Auto input, hc/io.go:172).
 // ---------------------------------------------------------------------------
-struct EncodeSmem {
-  uint32_t code[256];
-  uint32_t len[256];
-  uint64_t in_off[kWavesPerBlock][kLitsPerWave + 1];
-  uint64_t out_off[kWavesPerBlock][kLitsPerWave + 1];
+namespace enc {
+constexpr int kWaves = 8;
+constexpr int kThreads = kWave * kWaves;
+constexpr int kTileLits = 256;
+constexpr int kInCap = 8192;
+constexpr int kOutCap = 8192;
+
+struct LenWaveSmem {
+  uint32_t in_w[kInCap / 4 + 4];
+  uint32_t rec[kTileLits + 1];
 };
+struct LenSmem {
+  uint32_t len[256];
+  LenWaveSmem w[kWaves];
+};
+struct WaveSmem {
+  uint32_t in_w[kInCap / 4 + 4];
+  uint32_t out_w[kOutCap / 4 + 4];
+  uint2 rec[kTileLits + 1];
+};
+struct Smem {
+  uint2 code[256];  // (code left-aligned in 32 bits, length)
+  WaveSmem w[kWaves];
+};
+}  // namespace enc
 
-__global__ __launch_bounds__(kBlock) void encode_len_kernel(
+__device__ __forceinline__ uint32_t lds_byte(const uint32_t *w, uint32_t x) {
+  return (w[x >> 2] >> ((x & 3u) * 8u)) & 0xffu;
+}
+
+__global__ __launch_bounds__(enc::kThreads) void encode_len_kernel(
     const uint8_t *__restrict__ in, const uint64_t *__restrict__ in_off, uint64_t in_bias, uint64_t n,
-    uint32_t *__restrict__ enc_len, const uint8_t *__restrict__ g_len) {
-  __shared__ EncodeSmem sm;
+    uint32_t *__restrict__ enc_len, const uint8_t *__restrict__ g_len, uint64_t ntiles) {
+  using namespace enc;
+  __shared__ LenSmem sm;
   const int tid = threadIdx.x;
-  const int wave = tid / kWave;
+  const int wave = __builtin_amdgcn_readfirstlane(tid / kWave);
   const int lane = tid % kWave;
-  for (int i = tid; i < 256; i += kBlock) sm.len[i] = g_len[i];
-  const uint64_t s = ((uint64_t)blockIdx.x * kWavesPerBlock + wave) * kLitsPerWave;
-  const uint32_t cnt = s < n ? (uint32_t)min((uint64_t)kLitsPerWave, n - s) : 0u;
-  if (cnt) load_tile_offsets(in_off, s, cnt, sm.in_off[wave], lane);
+  for (int i = tid; i < 256; i += kThreads) sm.len[i] = g_len[i];
   __syncthreads();
-  if (!cnt) return;
-  const uint64_t *lin = sm.in_off[wave];
-  TileRun run;
-  split_runs(lin, cnt, lane, run);
-  for (uint32_t j = run.first; j < run.last; j++) {
-    const uint8_t *p = in + (lin[j] - in_bias);
-    const uint64_t L = lin[j + 1] - lin[j];
-    uint64_t bits = 0;
-    uint64_t i = 0;
-    // head bytes up to a 4-byte boundary, then whole words, then the tail
-    for (; i < L && (((uintptr_t)(p + i)) & 3u); i++) bits += sm.len[p[i]];
-    for (; i + 4 <= L; i += 4) {
-      const uint32_t w = *(const uint32_t *)(p + i);
-      bits += sm.len[w & 0xffu] + sm.len[(w >> 8) & 0xffu] + sm.len[(w >> 16) & 0xffu] + sm.len[w >> 24];
+  LenWaveSmem &ws = sm.w[wave];
+  const uint64_t stride = (uint64_t)gridDim.x * kWaves;
+  for (uint64_t t = (uint64_t)blockIdx.x * kWaves + wave; t < ntiles; t += stride) {
+    const uint64_t s = t * kTileLits;
+    const uint32_t cnt = (uint32_t)min((uint64_t)kTileLits, n - s);
+    TileOffsets<kTileLits> off;
+    off.load(in_off, nullptr, s, cnt, lane);
+    uint32_t cur = 0;
+    while (cur < cnt) {
+      const uint64_t ic = in_off[s + cur];
+      const uint8_t *ia = in + (ic - in_bias);
+      const uint32_t idelta = (uint32_t)((uintptr_t)ia & 15u);
+      const uint32_t end = off.fit(cur, cnt, ic, kInCap - idelta, 0, ~0ull, lane);
+      if (end == cur) {  // one huge literal: this lane sums it from global memory
+        if (lane == 0) {
+          const uint64_t L = in_off[s + cur + 1] - ic;
+          uint64_t bits = 0;
+          for (uint64_t i = 0; i < L; i++) bits += sm.len[ia[i]];
+          enc_len[s + cur] = (uint32_t)((bits + 7u) >> 3);
+        }
+        cur++;
+        continue;
+      }
+      const uint32_t m = end - cur;
+#pragma unroll
+      for (int k = 0; k < TileOffsets<kTileLits>::kPer; k++) {
+        const uint32_t j = (uint32_t)lane + (uint32_t)k * kWave;
+        if (j >= cur && j <= end) ws.rec[j - cur] = (uint32_t)(off.io[k] - ic) + idelta;
+      }
+      const uint32_t in_bytes = (uint32_t)(in_off[s + end] - ic) + idelta;
+      stage_in<false>(ws.in_w, ia - idelta, in_bytes, lane);
+      wave_sync();
+      uint32_t j, last;
+      lane_run([&](uint32_t i) { return ws.rec[i]; }, m, lane, j, last);
+      if (j < last) {
+        uint32_t x = ws.rec[j], xend = ws.rec[j + 1];
+        uint32_t bits = 0;
+        while (true) {
+          if (x < xend) {
+            // whole aligned words where possible
+            if ((x & 3u) == 0 && x + 4 <= xend) {
+              const uint32_t w = ws.in_w[x >> 2];
+              bits += sm.len[w & 0xffu] + sm.len[(w >> 8) & 0xffu] + sm.len[(w >> 16) & 0xffu] + sm.len[w >> 24];
+              x += 4;
+            } else {
+              bits += sm.len[lds_byte(ws.in_w, x)];
+              x++;
+            }
+          } else {
+            enc_len[s + cur + j] = (bits + 7u) >> 3;
+            if (++j >= last) break;
+            bits = 0;
+            xend = ws.rec[j + 1];
+          }
+        }
+      }
+      wave_sync();
+      cur = end;
     }
-    for (; i < L; i++) bits += sm.len[p[i]];
-    enc_len[s + j] = (uint32_t)((bits + 7u) >> 3);
   }
 }
 
 // ---------------------------------------------------------------------------
-// Encode: concatenated codes MSB-first, then Pad(0xff) (hc/huffman.go:23-37,
-// io/bitio.go:72-149).
+// Encode (hc/huffman.go:23-37 over io/bitio.go:72-149): codes MSB-first, the
+// last octet padded with 1 bits.  Output words are assembled in registers on
+// the LDS word grid and OR-ed into the zeroed staging area (a word may be
+// shared by two lanes at run boundaries, hence the OR).
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(kBlock) void encode_kernel(
+__global__ __launch_bounds__(enc::kThreads) void encode_kernel(
     const uint8_t *__restrict__ in, const uint64_t *__restrict__ in_off, uint64_t in_bias, uint64_t n,
     uint8_t *__restrict__ out, const uint64_t *__restrict__ out_off, uint64_t out_bias,
-    const uint32_t *__restrict__ g_code, const uint8_t *__restrict__ g_len) {
-  __shared__ EncodeSmem sm;
+    const uint32_t *__restrict__ g_code, const uint8_t *__restrict__ g_len, uint64_t ntiles) {
+  using namespace enc;
+  __shared__ Smem sm;
   const int tid = threadIdx.x;
-  const int wave = tid / kWave;
+  const int wave = __builtin_amdgcn_readfirstlane(tid / kWave);
   const int lane = tid % kWave;
-  for (int i = tid; i < 256; i += kBlock) {
-    sm.code[i] = g_code[i];
-    sm.len[i] = g_len[i];
-  }
-  const uint64_t s = ((uint64_t)blockIdx.x * kWavesPerBlock + wave) * kLitsPerWave;
-  const uint32_t cnt = s < n ? (uint32_t)min((uint64_t)kLitsPerWave, n - s) : 0u;
-  if (cnt) {
-    load_tile_offsets(in_off, s, cnt, sm.in_off[wave], lane);
-    load_tile_offsets(out_off, s, cnt, sm.out_off[wave], lane);
+  for (int i = tid; i < 256; i += kThreads) {
+    const uint32_t L = g_len[i];
+    sm.code[i] = make_uint2(g_code[i] << (32u - L), L);
   }
   __syncthreads();
-  if (!cnt) return;
-  const uint64_t *lin = sm.in_off[wave];
-  const uint64_t *lout = sm.out_off[wave];
-  TileRun run;
-  split_runs(lin, cnt, lane, run);
-  for (uint32_t j = run.first; j < run.last; j++) {
-    const uint8_t *p = in + (lin[j] - in_bias);
-    const uint64_t L = lin[j + 1] - lin[j];
-    uint8_t *dst = out + (lout[j] - out_bias);
-    const uint64_t cap = lout[j + 1] - lout[j];
-    uint64_t acc = 0;
-    uint32_t nacc = 0;
-    uint64_t o = 0;
-    for (uint64_t i = 0; i < L; i++) {
-      const uint32_t b = p[i];
-      acc = (acc << sm.len[b]) | sm.code[b];
-      nacc += sm.len[b];
-      while (nacc >= 8) {
-        nacc -= 8;
-        if (o < cap) dst[o] = (uint8_t)(acc >> nacc);
-        o++;
+  WaveSmem &ws = sm.w[wave];
+  const uint64_t stride = (uint64_t)gridDim.x * kWaves;
+  for (uint64_t t = (uint64_t)blockIdx.x * kWaves + wave; t < ntiles; t += stride) {
+    const uint64_t s = t * kTileLits;
+    const uint32_t cnt = (uint32_t)min((uint64_t)kTileLits, n - s);
+    TileOffsets<kTileLits> off;
+    off.load(in_off, out_off, s, cnt, lane);
+    uint32_t cur = 0;
+    while (cur < cnt) {
+      const uint64_t ic = in_off[s + cur], oc = out_off[s + cur];
+      const uint8_t *ia = in + (ic - in_bias);
+      uint8_t *oa = out + (oc - out_bias);
+      const uint32_t idelta = (uint32_t)((uintptr_t)ia & 15u);
+      const uint32_t odelta = (uint32_t)((uintptr_t)oa & 15u);
+      const uint32_t end = off.fit(cur, cnt, ic, kInCap - idelta, oc, kOutCap - odelta, lane);
+      if (end == cur) {  // one huge literal: lane 0 encodes it byte-serially to global memory
+        if (lane == 0) {
+          const uint64_t L = in_off[s + cur + 1] - ic, cap = out_off[s + cur + 1] - oc;
+          uint64_t acc = 0, o = 0;
+          uint32_t nacc = 0;
+          for (uint64_t i = 0; i < L; i++) {
+            const uint2 cl = sm.code[ia[i]];
+            acc = (acc << cl.y) | (cl.x >> (32u - cl.y));
+            nacc += cl.y;
+            while (nacc >= 8) {
+              nacc -= 8;
+              if (o < cap) oa[o] = (uint8_t)(acc >> nacc);
+              o++;
+            }
+          }
+          if (nacc && o < cap) oa[o] = (uint8_t)((acc << (8 - nacc)) | ((1u << (8 - nacc)) - 1u));
+        }
+        cur++;
+        continue;
       }
-    }
-    if (nacc) {  // Pad(0xff): the top 8-nacc bits of 0xff
-      const uint32_t padn = 8 - nacc;
-      if (o < cap) dst[o] = (uint8_t)((acc << padn) | ((1u << padn) - 1u));
+      const uint32_t m = end - cur;
+#pragma unroll
+      for (int k = 0; k < TileOffsets<kTileLits>::kPer; k++) {
+        const uint32_t j = (uint32_t)lane + (uint32_t)k * kWave;
+        if (j >= cur && j <= end)
+          ws.rec[j - cur] = make_uint2((uint32_t)(off.io[k] - ic) + idelta, (uint32_t)(off.oo[k] - oc) + odelta);
+      }
+      const uint32_t in_bytes = (uint32_t)(in_off[s + end] - ic) + idelta;
+      const uint32_t out_bytes = (uint32_t)(out_off[s + end] - oc) + odelta;
+      stage_in<false>(ws.in_w, ia - idelta, in_bytes, lane);
+      zero_lds((uint8_t *)ws.out_w, out_bytes, lane);
+      wave_sync();
+      uint32_t j, last;
+      lane_run([&](uint32_t i) { return ws.rec[i].x; }, m, lane, j, last);
+      if (j < last) {
+        uint2 r0 = ws.rec[j], r1 = ws.rec[j + 1];
+        uint32_t x = r0.x, xend = r1.x;
+        uint32_t bp = r0.y * 8u;            // absolute output bit position in the staging words
+        uint32_t obits_end = r1.y * 8u;     // end of this literal's region
+        uint64_t acc = 0;                   // bits of word bp>>5 onwards, MSB-aligned at bit 63
+        uint32_t *ow = ws.out_w;
+        while (true) {
+          if (x < xend) {
+            const uint2 cl = sm.code[lds_byte(ws.in_w, x)];
+            x++;
+            const uint32_t sh = bp & 31u;
+            acc |= ((uint64_t)cl.x << 32) >> sh;
+            bp += cl.y;
+            if (sh + cl.y >= 32u) {  // the word at the old position is complete
+              if (bp - cl.y < obits_end) atomicOr(&ow[(bp - cl.y) >> 5], __builtin_bswap32((uint32_t)(acc >> 32)));
+              acc <<= 32;
+            }
+          } else {
+            // Pad(0xff): fill to the octet boundary with 1 bits, then flush the partial word
+            const uint32_t pad = (8u - (bp & 7u)) & 7u;
+            const uint32_t sh = bp & 31u;
+            if (pad) acc |= ((((uint64_t)1 << pad) - 1u) << (64u - pad)) >> sh;
+            bp += pad;
+            if ((bp & 31u) != 0 || pad) {
+              const uint32_t wpos = (bp - 1u) >> 5;  // the word holding the last written bit
+              if (bp <= obits_end && ((bp & 31u) != 0 || sh != 0 || pad))
+                atomicOr(&ow[wpos], __builtin_bswap32((uint32_t)(acc >> 32)));
+            }
+            if (++j >= last) break;
+            r1 = ws.rec[j + 1];
+            x = xend;
+            xend = r1.x;
+            bp = obits_end;  // the next region starts where this one ends
+            obits_end = r1.y * 8u;
+            acc = 0;
+          }
+        }
+      }
+      wave_sync();
+      store_out(oa - odelta, (const uint8_t *)ws.out_w, odelta, out_bytes, lane);
+      wave_sync();
+      cur = end;
     }
   }
 }
@@ -414,9 +694,26 @@ hipError_t run_scan(F f, uint64_t n, uint64_t base, uint64_t *oa, uint64_t *ob, 
   return e != hipSuccess ? e : e2;
 }
 
-inline unsigned tiles_grid(uint64_t n) {
-  const uint64_t waves = (n + kLitsPerWave - 1) / kLitsPerWave;
-  return (unsigned)((waves + kWavesPerBlock - 1) / kWavesPerBlock);
+int g_cus = 0;
+
+inline int device_cus() {
+  if (g_cus == 0) {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) == hipSuccess &&
+        hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0)
+      g_cus = v;
+    else
+      g_cus = 256;
+  }
+  return g_cus;
+}
+
+// Persistent-style grid: at most one workgroup per CU per `per_cu`, never more
+// workgroups than tiles need.
+inline unsigned tile_grid(uint64_t ntiles, int waves, int per_cu) {
+  const uint64_t want = (ntiles + waves - 1) / waves;
+  const uint64_t cap = (uint64_t)device_cus() * per_cu;
+  return (unsigned)(want < cap ? want : cap);
 }
 
 }  // namespace
@@ -425,23 +722,27 @@ hipError_t launch_decode(const DevTables &t, const uint8_t *in, const uint64_t *
                          uint64_t n, uint8_t *out, const uint64_t *out_off, uint64_t out_bias,
                          uint32_t *out_len, uint8_t *status, hipStream_t s) {
   if (n == 0) return hipSuccess;
-  decode_kernel<<<dim3(tiles_grid(n)), dim3(kBlock), 0, s>>>(in, in_off, in_bias, n, out, out_off, out_bias,
-                                                            out_len, status, t.lut1, t.lut2);
+  const uint64_t ntiles = (n + dec::kTileLits - 1) / dec::kTileLits;
+  decode_kernel<<<dim3(tile_grid(ntiles, dec::kWaves, 1)), dim3(dec::kThreads), 0, s>>>(
+      in, in_off, in_bias, n, out, out_off, out_bias, out_len, status, t.lut1, t.lut2, ntiles);
   return hipGetLastError();
 }
 
 hipError_t launch_encode_len(const DevTables &t, const uint8_t *in, const uint64_t *in_off, uint64_t in_bias,
                              uint64_t n, uint32_t *enc_len, hipStream_t s) {
   if (n == 0) return hipSuccess;
-  encode_len_kernel<<<dim3(tiles_grid(n)), dim3(kBlock), 0, s>>>(in, in_off, in_bias, n, enc_len, t.len);
+  const uint64_t ntiles = (n + enc::kTileLits - 1) / enc::kTileLits;
+  encode_len_kernel<<<dim3(tile_grid(ntiles, enc::kWaves, 2)), dim3(enc::kThreads), 0, s>>>(
+      in, in_off, in_bias, n, enc_len, t.len, ntiles);
   return hipGetLastError();
 }
 
 hipError_t launch_encode(const DevTables &t, const uint8_t *in, const uint64_t *in_off, uint64_t in_bias,
                          uint64_t n, uint8_t *out, const uint64_t *out_off, uint64_t out_bias, hipStream_t s) {
   if (n == 0) return hipSuccess;
-  encode_kernel<<<dim3(tiles_grid(n)), dim3(kBlock), 0, s>>>(in, in_off, in_bias, n, out, out_off, out_bias,
-                                                            t.code, t.len);
+  const uint64_t ntiles = (n + enc::kTileLits - 1) / enc::kTileLits;
+  encode_kernel<<<dim3(tile_grid(ntiles, enc::kWaves, 1)), dim3(enc::kThreads), 0, s>>>(
+      in, in_off, in_bias, n, out, out_off, out_bias, t.code, t.len, ntiles);
   return hipGetLastError();
 }
 
