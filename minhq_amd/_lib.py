@@ -10,7 +10,7 @@ import ctypes as C
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libmhq_huff.so")
+LIB_PATH = os.environ.get("MHQ_LIB_PATH") or os.path.join(HERE, "libmhq_huff.so")
 
 MHQ_OK = 0
 MHQ_EINVAL = -22

@@ -150,8 +150,8 @@ constexpr int kOutCap = 8192;  // staged output bytes per wave
 
 struct WaveSmem {
   uint32_t in_w[kInCap / 4 + 4];  // byte-swapped input words (+ tail for window reads)
-  uint8_t out_b[kOutCap + kWave]; // output staging (+ one junk byte per lane)
-  uint2 rec[kTileLits + 1];       // per boundary: (input byte index, output byte index)
+  uint8_t out_b[kOutCap + 16];    // output staging (+ one spare word pair)
+  uint2 rec[kTileLits + 2];       // per boundary: (input byte index, output byte index)
   uint32_t olen[kTileLits];       // out_len | status << 31
 };
 struct Smem {
@@ -266,62 +266,71 @@ __global__ __launch_bounds__(dec::kThreads) void decode_kernel(
 
       uint32_t j, last;
       lane_run([&](uint32_t i) { return ws.rec[i].x; }, m, lane, j, last);
+#ifdef MHQ_DIAG_NO_DECODE  // diagnostic build: staging and stores only
+      for (uint32_t i = j; i < last; i++) ws.olen[i] = ws.rec[i + 1].y - ws.rec[i].y;
+      j = last;
+#endif
       if (j < last) {
-        uint32_t p = ws.rec[j].x * 8u;
+        // Lane state.  Output bytes are packed into registers on the LDS word
+        // grid and OR-ed into the zeroed staging words: a lane only ever ORs
+        // its own bytes (zeros elsewhere), so words shared with a neighbouring
+        // lane at run boundaries need no ordering.
+        uint32_t p = ws.rec[j].x * 8u;  // next code's bit position
         uint2 r = ws.rec[j + 1];
-        uint32_t endbit = r.x * 8u;
+        uint32_t endbit = r.x * 8u;     // end of this literal
         uint32_t optr = ws.rec[j].y, ostart = optr, oend = r.y;
-        const uint32_t junk = kOutCap + (uint32_t)lane;
-        while (true) {
-          const uint32_t rem = endbit - p;
-          const uint32_t k = p >> 5, sh = p & 31u;
-          const uint32_t w0 = ws.in_w[k], w1 = ws.in_w[k + 1];
-          const uint32_t win = sh ? __builtin_amdgcn_alignbit(w0, w1, 32u - sh) : w0;
-          const uint32_t e = lut1[win >> (32 - kLut1Bits)];
-          uint32_t cnt_s, adv, syms, bad = 0;
-          if (e >> 26) {  // one or two codes of <= 12 bits
-            const uint32_t len0 = (e >> 16) & 31u, tot = (e >> 21) & 31u;
-            const bool both = tot <= rem;
-            cnt_s = both ? (e >> 26) : (len0 <= rem ? 1u : 0u);
-            adv = both ? tot : len0;
-            syms = e;
-          } else {  // a code of 13..30 bits, or the all-ones EOS prefix
-            const uint32_t nw = ~win;
-            const uint32_t c = nw ? (uint32_t)__builtin_clz(nw) : 32u;
-            if (c >= (uint32_t)kEosOnes) {
-              cnt_s = 0;
-              adv = 0;
-              syms = 0;
-              bad = rem > (uint32_t)kEosOnes;  // a 31st bit exists: nil child
-            } else {
-              const uint32_t e2 = lut2[(c << kLut2SubBits) | ((win << (c + 1)) >> (32 - kLut2SubBits))];
-              const uint32_t L = e2 >> 8;
-              cnt_s = (L != 0 && L <= rem) ? 1u : 0u;
-              adv = L;
-              syms = e2 & 0xffu;
+        uint32_t acc = 0;               // this lane's bytes of word optr>>2 below optr
+        uint32_t bad = 0;
+        uint32_t *ow = (uint32_t *)ws.out_b;
+        while (j < last) {
+          const uint32_t w0 = optr >> 2;
+          uint64_t o64 = acc;
+          bool fin = false;
+#pragma unroll
+          for (int u = 0; u < 2; u++) {  // two probes per iteration, one output flush
+            const uint32_t k = p >> 5, sh = p & 31u;
+            const uint64_t ww = ((uint64_t)ws.in_w[k] << 32) | ws.in_w[k + 1];
+            const uint32_t win = (uint32_t)((ww << sh) >> 32);
+            const uint32_t e = lut1[win >> (32 - kLut1Bits)];
+            const uint32_t rem = endbit - p;
+            uint32_t len0 = (e >> 16) & 31u, tot = (e >> 21) & 31u, ns = e >> 26, syms = e & 0xffffu;
+            if (ns == 0) {  // a code of 13..30 bits, or the all-ones EOS prefix
+              const uint32_t nw = ~win;
+              const uint32_t c = nw ? (uint32_t)__builtin_clz(nw) : 32u;
+              if (c >= (uint32_t)kEosOnes) {
+                len0 = tot = 0xffffffffu;       // never fits: the literal ends here
+                bad |= rem > (uint32_t)kEosOnes;  // a 31st bit exists: nil child
+              } else {
+                const uint32_t e2 = lut2[(c << kLut2SubBits) | ((win << (c + 1)) >> (32 - kLut2SubBits))];
+                len0 = tot = (e2 >> 8) ? (e2 >> 8) : 0xffffffffu;
+                ns = 1;
+                syms = e2 & 0xffu;
+              }
             }
+            const bool ct = tot <= rem;
+            uint32_t cnt = ct ? ns : (len0 <= rem ? 1u : 0u);
+            const uint32_t adv = ct ? tot : len0;
+            const uint32_t room = oend - optr;  // Read() stops once p is full (hc/huffman.go:104)
+            cnt = cnt < room ? cnt : room;
+            o64 |= (uint64_t)__builtin_amdgcn_ubfe(syms, 0, cnt * 8u) << ((optr - 4u * w0) * 8u);
+            optr += cnt;
+            p += cnt ? adv : 0u;
+            fin |= cnt == 0;
           }
-          // Read() returns as soon as its buffer is full (hc/huffman.go:104)
-          const uint32_t room = oend - optr;
-          if (room == 0) {
-            cnt_s = 0;
-            bad = 0;
-          } else if (cnt_s > room) {
-            cnt_s = room;
-          }
-          ws.out_b[cnt_s >= 1 ? optr : junk] = (uint8_t)syms;
-          ws.out_b[cnt_s >= 2 ? optr + 1 : junk] = (uint8_t)(syms >> 8);
-          optr += cnt_s;
-          if (cnt_s == 0) {  // end of this literal
+          atomicOr(&ow[w0], (uint32_t)o64);
+          atomicOr(&ow[w0 + 1], (uint32_t)(o64 >> 32));
+          acc = (optr >> 2) != w0 ? (uint32_t)(o64 >> 32) : (uint32_t)o64;
+          if (fin) {  // end of this literal (EOF, full buffer or invalid code)
+            bad = optr != oend ? bad : 0u;
             ws.olen[j] = (optr - ostart) | (bad << 31);
-            if (++j >= last) break;
-            p = endbit;
+            j++;
+            bad = 0;
             r = ws.rec[j + 1];
+            p = endbit;
             endbit = r.x * 8u;
-            ostart = optr = oend;
+            if ((oend >> 2) != (optr >> 2)) acc = 0;  // bytes below the next region are slack
+            optr = ostart = oend;
             oend = r.y;
-          } else {
-            p += adv;
           }
         }
       }

@@ -1,0 +1,125 @@
+#!/usr/bin/env python3
+"""Minimal driver for profiling one kernel of libmhq_huff.so.
+
+    python tools/kernel_driver.py --kernel decode --config northstar --iters 50
+
+Prepares the batch on the device (encoding it first for decode), then times
+`--iters` launches over rotating buffer copies (>= 1 GiB) with HIP events, and
+prints one JSON line.  Meant to run under `rocprofv3 --kernel-trace` or
+`--pmc`; MHQ_LIB_PATH may point at a variant build.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def batch_for(name: str, n: int):
+    from minhq_amd import workloads as w
+
+    if name == "northstar":
+        return w.north_star(n or (1 << 20))
+    if name == "config2":
+        return w.config2(n or (1 << 20))
+    if name == "config2print":
+        return w.config2(n or (1 << 20), "print")
+    if name == "config4":
+        return w.config4(n or (1 << 22))
+    if name == "config5":
+        return w.config5(n or (1 << 20))
+    raise SystemExit(f"unknown config {name}")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--kernel", default="decode", choices=["decode", "encode", "encode_len", "offsets"])
+    ap.add_argument("--config", default="northstar")
+    ap.add_argument("--n", type=int, default=0)
+    ap.add_argument("--iters", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--rotate-gib", type=float, default=1.0)
+    args = ap.parse_args()
+
+    import torch
+
+    from minhq_amd import hc
+
+    b = batch_for(args.config, args.n)
+    dev = torch.device("cuda:0")
+    codec = hc.Codec(devices=[0])
+    n = b.n
+    data = torch.from_numpy(b.data).to(dev)
+    off = torch.from_numpy(b.off.view(np.int64)).to(dev)
+    enc_len = torch.empty(n, dtype=torch.int32, device=dev)
+    enc_off = torch.empty(n + 1, dtype=torch.int64, device=dev)
+    cap_off = torch.empty(n + 1, dtype=torch.int64, device=dev)
+    codec.encode_len_dev(data, off, enc_len)
+    codec.offsets_dev(enc_len, enc_off, cap_off)
+    torch.cuda.synchronize()
+    enc_bytes = int(enc_off[-1].item())
+    cap_bytes = int(cap_off[-1].item())
+    enc = torch.empty(enc_bytes + 16, dtype=torch.uint8, device=dev)
+    codec.encode_dev(data, off, enc, enc_off)
+    torch.cuda.synchronize()
+
+    per = {"decode": enc_bytes + cap_bytes + 16 * n, "encode": b.nbytes + enc_bytes + 16 * n,
+           "encode_len": b.nbytes + 12 * n, "offsets": 20 * n}[args.kernel]
+    R = max(2, int(np.ceil(args.rotate_gib * (1 << 30) / per)))
+    slots = []
+    for _ in range(R):
+        s = {}
+        if args.kernel == "decode":
+            s["in"], s["off"], s["cap"] = enc.clone(), enc_off.clone(), cap_off.clone()
+            s["out"] = torch.empty(cap_bytes + 16, dtype=torch.uint8, device=dev)
+            s["len"] = torch.empty(n, dtype=torch.int32, device=dev)
+            s["st"] = torch.empty(n, dtype=torch.uint8, device=dev)
+        elif args.kernel in ("encode", "encode_len"):
+            s["in"], s["off"], s["eoff"] = data.clone(), off.clone(), enc_off.clone()
+            s["out"] = torch.empty(enc_bytes + 16, dtype=torch.uint8, device=dev)
+            s["len"] = torch.empty(n, dtype=torch.int32, device=dev)
+        else:
+            s["len"] = enc_len.clone()
+            s["o1"] = torch.empty_like(enc_off)
+            s["o2"] = torch.empty_like(cap_off)
+        slots.append(s)
+
+    def run(s):
+        if args.kernel == "decode":
+            codec.decode_dev(s["in"], s["off"], s["out"], s["cap"], s["len"], s["st"])
+        elif args.kernel == "encode":
+            codec.encode_dev(s["in"], s["off"], s["out"], s["eoff"])
+        elif args.kernel == "encode_len":
+            codec.encode_len_dev(s["in"], s["off"], s["len"])
+        else:
+            codec.offsets_dev(s["len"], s["o1"], s["o2"])
+
+    for i in range(args.warmup):
+        run(slots[i % R])
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for i in range(args.iters):
+        run(slots[i % R])
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / args.iters
+    if args.kernel == "decode":
+        s = slots[0]
+        assert int(s["st"].sum().item()) == 0
+        assert torch.equal(s["len"].long(), off[1:] - off[:-1])
+    alg = {"decode": enc_bytes + b.nbytes + 16 * (n + 1) + 5 * n,
+           "encode": b.nbytes + enc_bytes + 16 * (n + 1),
+           "encode_len": b.nbytes + 8 * (n + 1) + 4 * n, "offsets": 4 * n + 16 * (n + 1)}[args.kernel]
+    print(json.dumps({"kernel": args.kernel, "config": b.name, "n": n, "plain": b.nbytes, "enc": enc_bytes,
+                      "us_per_launch": round(ms * 1e3, 2), "plain_gib_s": round(b.nbytes / ms / 1e6 / 1.073741824, 2),
+                      "alg_bytes": alg, "hbm_frac": round(alg / (ms / 1e3) / 8e12, 4), "rotating": R}))
+
+
+if __name__ == "__main__":
+    main()
