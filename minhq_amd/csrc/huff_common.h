@@ -1,0 +1,167 @@
+// huff_common.h -- device helpers shared by the gfx950 codec kernels.
+//
+// Tiles: every kernel walks tiles of consecutive literals, one tile per wave
+// at a time.  A tile's offsets come in as coalesced u64 loads (kept in
+// registers, lane + 64k), its bytes are staged into the wave's LDS slice with
+// aligned 16-B loads, and outputs leave the LDS slice as aligned 16-B stores.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace mhq {
+namespace dev {
+
+constexpr int kWave = 64;
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+// Orders this wave's LDS accesses (they retire in order per wave; this keeps
+// the compiler from moving them across a phase boundary).
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __forceinline__ uint32_t popc64(uint64_t m) { return (uint32_t)__popcll(m); }
+
+template <int kTileLits>
+struct TileOffsets {
+  static constexpr int kPer = (kTileLits + 1 + kWave - 1) / kWave;
+  uint64_t io[kPer];  // in_off[s + lane + 64k]
+  uint64_t oo[kPer];  // out_off[s + lane + 64k] (unused by encode_len)
+
+  __device__ __forceinline__ void load(const uint64_t *__restrict__ in_off, const uint64_t *__restrict__ out_off,
+                                       uint64_t s, uint32_t cnt, int lane) {
+#pragma unroll
+    for (int k = 0; k < kPer; k++) {
+      const uint32_t j = (uint32_t)lane + (uint32_t)k * kWave;
+      io[k] = j <= cnt ? __builtin_nontemporal_load(in_off + s + j) : 0;
+      oo[k] = (out_off && j <= cnt) ? __builtin_nontemporal_load(out_off + s + j) : 0;
+    }
+  }
+
+  // Literals [cur, end] fit when their input span (from the 16-B aligned start)
+  // is <= in_lim and their output span <= out_lim.  Returns end (>= cur; == cur
+  // means literal `cur` alone does not fit).
+  __device__ __forceinline__ uint32_t fit(uint32_t cur, uint32_t cnt, uint64_t in_lo, uint64_t in_lim,
+                                          uint64_t out_lo, uint64_t out_lim, int lane) const {
+    uint32_t n = 0;
+#pragma unroll
+    for (int k = 0; k < kPer; k++) {
+      const uint32_t j = (uint32_t)lane + (uint32_t)k * kWave;
+      const bool ok = j > cur && j <= cnt && (io[k] - in_lo) <= in_lim && (oo[k] - out_lo) <= out_lim;
+      n += popc64(__ballot(ok));
+    }
+    return cur + n;
+  }
+};
+
+// First index i in [0, m) with key(i) >= target, or m.
+template <class K>
+__device__ __forceinline__ uint32_t lower_bound(K key, uint32_t m, uint32_t target) {
+  uint32_t lo = 0, hi = m;
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (key(mid) < target) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo;
+}
+
+// Byte-balanced split of literals [0, m) (input byte starts key(i)) into 64
+// contiguous runs, one per lane.
+template <class K>
+__device__ __forceinline__ void lane_run(K key, uint32_t m, int lane, uint32_t &first, uint32_t &last) {
+  const uint32_t b0 = key(0);
+  const uint32_t total = key(m) - b0;
+  const uint32_t t0 = b0 + (uint32_t)(((uint64_t)total * (uint32_t)lane) >> 6);
+  const uint32_t t1 = b0 + (uint32_t)(((uint64_t)total * (uint32_t)(lane + 1)) >> 6);
+  first = lane == 0 ? 0u : lower_bound(key, m, t0);
+  last = lane == kWave - 1 ? m : lower_bound(key, m, t1);
+}
+
+// Ascending bitonic sort of 128 keys held two per lane: element i lives in
+// lane i & 63, slot i >> 6 (v0: i = lane, v1: i = lane + 64).
+__device__ __forceinline__ void sort128(uint32_t &v0, uint32_t &v1, int lane) {
+#pragma unroll
+  for (int k = 2; k <= 128; k <<= 1) {
+#pragma unroll
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      if (j == 64) {
+        const uint32_t lo = v0 < v1 ? v0 : v1, hi = v0 < v1 ? v1 : v0;
+        v0 = lo;
+        v1 = hi;
+      } else {
+        const uint32_t o0 = __shfl_xor(v0, j), o1 = __shfl_xor(v1, j);
+        const bool lower = (lane & j) == 0;          // i < partner
+        const bool asc0 = (lane & k) == 0;            // element lane
+        const bool asc1 = ((lane + 64) & k) == 0;     // element lane + 64
+        const bool min0 = lower == asc0, min1 = lower == asc1;
+        v0 = min0 ? (v0 < o0 ? v0 : o0) : (v0 < o0 ? o0 : v0);
+        v1 = min1 ? (v1 < o1 ? v1 : o1) : (v1 < o1 ? o1 : v1);
+      }
+    }
+  }
+}
+
+// Copies global bytes [a, a+nbytes) (a 16-B aligned) into LDS words; kSwap
+// byte-swaps every word (MSB-first bit streams); kReverse stores logical word
+// w at index nwords-1-w so that {w+1, w} is one little-endian u64 pair.
+template <bool kSwap, bool kReverse>
+__device__ __forceinline__ void stage_in(uint32_t *lds, uint32_t nwords, const uint8_t *a, uint32_t nbytes,
+                                         int lane) {
+  const uint32_t chunks = (nbytes + 15u) >> 4;
+  const u32x4 *src = (const u32x4 *)a;
+  for (uint32_t c = lane; c < chunks; c += kWave) {
+    u32x4 v = __builtin_nontemporal_load(src + c);  // an aligned chunk holding a valid byte never crosses a page
+    if (kSwap) {
+      v.x = __builtin_bswap32(v.x);
+      v.y = __builtin_bswap32(v.y);
+      v.z = __builtin_bswap32(v.z);
+      v.w = __builtin_bswap32(v.w);
+    }
+    if (kReverse) {
+      *(u32x4 *)(lds + nwords - 4u - 4u * c) = v.wzyx;
+    } else {
+      *(u32x4 *)(lds + 4u * c) = v;
+    }
+  }
+}
+
+__device__ __forceinline__ void zero_lds(uint32_t *lds, uint32_t nbytes, int lane) {
+  const uint32_t chunks = (nbytes + 15u) >> 4;
+  for (uint32_t c = lane; c < chunks; c += kWave) *(u32x4 *)(lds + 4u * c) = u32x4{0u, 0u, 0u, 0u};
+}
+
+// Writes LDS bytes [lo, hi) to global o_al + [lo, hi), o_al 16-B aligned.
+// Whole 16-B chunks go out as one aligned store; the (at most two) partial
+// chunks at the ends are written byte by byte so neighbours are untouched.
+__device__ __forceinline__ void store_out(uint8_t *o_al, const uint8_t *lds, uint32_t lo, uint32_t hi, int lane) {
+  if (hi <= lo) return;
+  const uint32_t c0 = lo >> 4, c1 = (hi + 15u) >> 4;
+  for (uint32_t c = c0 + lane; c < c1; c += kWave) {
+    const uint32_t a = c << 4, b = a + 16u;
+    if (a >= lo && b <= hi) {
+      __builtin_nontemporal_store(*(const u32x4 *)(lds + a), (u32x4 *)(o_al + a));
+    } else {
+      const uint32_t x0 = a > lo ? a : lo, x1 = b < hi ? b : hi;
+      for (uint32_t x = x0; x < x1; x++) o_al[x] = lds[x];
+    }
+  }
+}
+
+__device__ __forceinline__ uint32_t lds_byte(const uint32_t *w, uint32_t x) {
+  return (w[x >> 2] >> ((x & 3u) * 8u)) & 0xffu;
+}
+
+int device_cus();
+// Persistent-style grid: at most `per_cu` workgroups per CU, never more than
+// the tiles need.
+inline unsigned tile_grid(uint64_t ntiles, int waves, int per_cu) {
+  const uint64_t want = (ntiles + waves - 1) / waves;
+  const uint64_t cap = (uint64_t)device_cus() * per_cu;
+  return (unsigned)(want < cap ? want : cap);
+}
+
+}  // namespace dev
+}  // namespace mhq

@@ -44,6 +44,7 @@ def main():
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--rotate-gib", type=float, default=1.0)
+    ap.add_argument("--no-check", action="store_true")
     args = ap.parse_args()
 
     import torch
@@ -102,6 +103,14 @@ def main():
     for i in range(args.warmup):
         run(slots[i % R])
     torch.cuda.synchronize()
+    import ctypes
+
+    from minhq_amd import _lib
+
+    diag = getattr(_lib.load(), "mhq_diag_read", None)
+    buf = (ctypes.c_ulonglong * 8)()
+    if diag:
+        diag(buf, 8)  # reset
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
     for i in range(args.iters):
@@ -109,7 +118,14 @@ def main():
     e1.record()
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / args.iters
-    if args.kernel == "decode":
+    if diag:
+        diag(buf, 8)
+        tot = sum(buf[:5]) or 1
+        print("diag phases (share of wave cycles): " + " ".join(
+            f"{nm}={buf[i] / tot:.3f}" for i, nm in enumerate(["offs_fit", "stage", "split", "decode", "store"])),
+            f"wave-cycles/launch={tot / args.iters:.3g} decode-iters/launch={buf[5] / args.iters:.4g}"
+            f" cycles/iter={buf[3] / max(buf[5], 1):.1f}", file=sys.stderr)
+    if args.kernel == "decode" and not args.no_check:
         s = slots[0]
         assert int(s["st"].sum().item()) == 0
         assert torch.equal(s["len"].long(), off[1:] - off[:-1])
