@@ -32,11 +32,11 @@
 #include "huff_kernels.h"
 #include "huff_table.h"
 
-#ifndef MHQ_DEC_WAVES
-#define MHQ_DEC_WAVES 8
-#define MHQ_DEC_TILE 256
-#define MHQ_DEC_INCAP 6080
-#define MHQ_DEC_OUTCAP 8192
+#ifndef MHQ_DEC_WAVES  // geometry (measured on MI355X: 16 waves/CU x 128-literal tiles is fastest)
+#define MHQ_DEC_WAVES 16
+#define MHQ_DEC_TILE 128
+#define MHQ_DEC_INCAP 3072
+#define MHQ_DEC_OUTCAP 3840
 #endif
 
 namespace mhq {
@@ -50,7 +50,10 @@ constexpr int kTileLits = MHQ_DEC_TILE;
 constexpr int kInCap = MHQ_DEC_INCAP;    // staged input bytes per wave (incl. 16-B alignment slack)
 constexpr int kOutCap = MHQ_DEC_OUTCAP;  // staged output bytes per wave
 constexpr uint32_t kInWords = kInCap / 4 + 4;
-constexpr int kStreams = 2;              // per lane
+#ifndef MHQ_DEC_STREAMS
+#define MHQ_DEC_STREAMS 1
+#endif
+constexpr int kStreams = MHQ_DEC_STREAMS;  // per lane (1 or 2)
 constexpr uint32_t kK = kWave * kStreams;
 constexpr int kBuckets = 64;
 constexpr uint32_t kNone = 0xffffffffu;
@@ -176,12 +179,14 @@ struct Stream {
     optr = ostart = r0.y;
     oend = r1.y;
     bad = 0;
+#ifdef MHQ_DEC_BITBUF
     const uint32_t k = p >> 5, sh = p & 31u;
     const uint64_t pair = ((uint64_t)in_word(ws, k) << 32) | in_word(ws, k + 1);
     bb = pair << sh;
     nb = 64u - sh;
     wi = k + 2u;
     nxt = in_word(ws, wi);
+#endif
   }
 };
 
@@ -199,8 +204,22 @@ struct Probe {
   uint32_t win, e, len0, tot, ns, syms;
 };
 
-__device__ __forceinline__ void probe_fast(Probe &q, const Stream &s, const uint32_t *lut1) {
+#ifndef MHQ_DEC_BITBUF
+// The 32 stream bits at bit position p (one ds_read2_b32 of logical words k, k+1).
+__device__ __forceinline__ uint32_t window_at(const WaveSmem &ws, uint32_t p) {
+  const uint32_t k = p >> 5, sh = p & 31u;
+  const uint32_t *wp = ws.in_w + (kInWords - 2u - k);
+  const uint64_t ww = (uint64_t)wp[0] | ((uint64_t)wp[1] << 32);  // {word k+1, word k}
+  return (uint32_t)((ww << sh) >> 32);
+}
+#endif
+
+__device__ __forceinline__ void probe_fast(Probe &q, const Stream &s, const WaveSmem &ws, const uint32_t *lut1) {
+#ifdef MHQ_DEC_BITBUF
   q.win = (uint32_t)(s.bb >> 32);
+#else
+  q.win = window_at(ws, s.p);
+#endif
   q.e = lut1[q.win >> (32 - kLut1Bits)];
   q.len0 = (q.e >> 16) & 31u;
   q.tot = (q.e >> 21) & 31u;
@@ -235,6 +254,9 @@ __device__ __forceinline__ void apply(const Probe &q, Stream &s, const WaveSmem 
   s.o64 |= (uint64_t)__builtin_amdgcn_ubfe(q.syms, 0, cnt * 8u) << ((s.optr - 4u * s.w0) * 8u);
   s.optr += cnt;
   s.fin |= cnt == 0;
+#ifndef MHQ_DEC_BITBUF
+  s.p += adv;
+#else
   // consume adv bits, then top the buffer up to >= 32 bits from the prefetched word
   s.bb <<= adv;
   s.nb -= adv;
@@ -244,6 +266,7 @@ __device__ __forceinline__ void apply(const Probe &q, Stream &s, const WaveSmem 
   s.nb += need ? 32u : 0u;
   s.wi += need ? 1u : 0u;
   s.nxt = in_word(ws, s.wi);
+#endif
 }
 
 __device__ __forceinline__ void flush(Stream &s, WaveSmem &ws) {
@@ -279,8 +302,8 @@ __device__ __forceinline__ void iter2(Stream &a, Stream &b, WaveSmem &ws, const 
 #pragma unroll
   for (int u = 0; u < 2; u++) {
     Probe qa, qb;
-    probe_fast(qa, a, lut1);
-    probe_fast(qb, b, lut1);
+    probe_fast(qa, a, ws, lut1);
+    probe_fast(qb, b, ws, lut1);
 #ifndef MHQ_DIAG_NO_LONG
     if (qa.ns == 0) probe_long(qa, a, lut2);
     if (qb.ns == 0) probe_long(qb, b, lut2);
@@ -292,6 +315,23 @@ __device__ __forceinline__ void iter2(Stream &a, Stream &b, WaveSmem &ws, const 
   flush(b, ws);
   if (a.fin && a.active()) finish(a, ws, ka, m);
   if (b.fin && b.active()) finish(b, ws, kb, m);
+}
+
+// Two probes for one stream (kStreams == 1).
+__device__ __forceinline__ void iter1(Stream &a, WaveSmem &ws, const uint32_t *lut1, const uint16_t *lut2,
+                                      uint32_t ka, uint32_t m) {
+  a.w0 = a.optr >> 2;
+  a.o64 = a.acc;
+  a.fin = false;
+#pragma unroll
+  for (int u = 0; u < 2; u++) {
+    Probe qa;
+    probe_fast(qa, a, ws, lut1);
+    if (qa.ns == 0) probe_long(qa, a, lut2);
+    apply(qa, a, ws);
+  }
+  flush(a, ws);
+  if (a.fin && a.active()) finish(a, ws, ka, m);
 }
 
 // Counting sort of literals [0, m) by encoded length (bucketed) into ws.order.
@@ -393,7 +433,8 @@ __global__ __launch_bounds__(kThreads) void decode_kernel(
       a.i = 0;
       b.i = 0;
       a.start(ws, next_literal_of(ws, ka, 0, m));
-      b.start(ws, next_literal_of(ws, kb, 0, m));
+      if (kStreams == 2) b.start(ws, next_literal_of(ws, kb, 0, m));
+      else b.start(ws, kNone);
 #ifdef MHQ_DIAG_ONE_STREAM  // diagnostic build: only stream a works (wrong output)
       b.start(ws, kNone);
 #endif
@@ -402,7 +443,8 @@ __global__ __launch_bounds__(kThreads) void decode_kernel(
 #endif
       STAMP(2);
       while (a.active() || b.active()) {
-        iter2(a, b, ws, lut1, lut2, ka, kb, m);
+        if (kStreams == 2) iter2(a, b, ws, lut1, lut2, ka, kb, m);
+        else iter1(a, ws, lut1, lut2, ka, m);
 #ifdef MHQ_DIAG_STAMPS
         ph[5]++;
 #endif
