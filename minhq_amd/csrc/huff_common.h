@@ -136,10 +136,12 @@ __device__ __forceinline__ void zero_lds(uint32_t *lds, uint32_t nbytes, int lan
 // Writes LDS bytes [lo, hi) to global o_al + [lo, hi), o_al 16-B aligned.
 // Whole 16-B chunks go out as one aligned store; the (at most two) partial
 // chunks at the ends are written byte by byte so neighbours are untouched.
-__device__ __forceinline__ void store_out(uint8_t *o_al, const uint8_t *lds, uint32_t lo, uint32_t hi, int lane) {
+// `lane` / `nthreads`: this thread's index among the threads sharing the copy.
+__device__ __forceinline__ void store_out(uint8_t *o_al, const uint8_t *lds, uint32_t lo, uint32_t hi, int lane,
+                                          uint32_t nthreads = kWave) {
   if (hi <= lo) return;
   const uint32_t c0 = lo >> 4, c1 = (hi + 15u) >> 4;
-  for (uint32_t c = c0 + lane; c < c1; c += kWave) {
+  for (uint32_t c = c0 + lane; c < c1; c += nthreads) {
     const uint32_t a = c << 4, b = a + 16u;
     if (a >= lo && b <= hi) {
       __builtin_nontemporal_store(*(const u32x4 *)(lds + a), (u32x4 *)(o_al + a));
@@ -155,6 +157,10 @@ __device__ __forceinline__ uint32_t lds_byte(const uint32_t *w, uint32_t x) {
 }
 
 int device_cus();
+
+#ifndef MHQ_PER_CU  // workgroups per CU in a tile grid (waves then loop over tiles)
+#define MHQ_PER_CU 1
+#endif
 // Persistent-style grid: at most `per_cu` workgroups per CU, never more than
 // the tiles need.
 inline unsigned tile_grid(uint64_t ntiles, int waves, int per_cu) {
