@@ -67,13 +67,9 @@ def barrier(pg):
 
 
 def max_over_ranks(pg, x: float) -> float:
-    if pg is None:
-        return x
-    import torch
+    from minhq_amd import shard
 
-    t = torch.tensor([x], dtype=torch.float64, device="cuda")
-    pg.all_reduce(t, op=pg.ReduceOp.MAX)
-    return float(t.item())
+    return shard.max_over_ranks(pg, x, "cuda")
 
 
 class Slot:

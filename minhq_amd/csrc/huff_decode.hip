@@ -34,8 +34,9 @@
 #include "huff_kernels.h"
 #include "huff_table.h"
 
-#ifndef MHQ_DEC_T  // threads (= literals) per block tile, and the staging slices
-#define MHQ_DEC_T 768
+#ifndef MHQ_DEC_T  // threads per block, literals per thread, and the staging slices
+#define MHQ_DEC_T 384
+#define MHQ_DEC_LPT 2
 #define MHQ_DEC_INCAP 20480
 #define MHQ_DEC_OUTCAP 30720
 #endif
@@ -49,6 +50,8 @@ namespace {
 using namespace dev;
 
 constexpr int kT = MHQ_DEC_T;
+constexpr int kLPT = MHQ_DEC_LPT;  // 1 or 2
+constexpr int kL = kT * kLPT;      // literals per block tile
 constexpr int kInCap = MHQ_DEC_INCAP;    // staged input bytes (incl. 16-B alignment slack)
 constexpr int kOutCap = MHQ_DEC_OUTCAP;  // staged output bytes
 constexpr uint32_t kInWords = kInCap / 4 + 4;
@@ -59,9 +62,9 @@ struct Smem {
   uint16_t lut2[kLut2Size];
   uint32_t in_w[kInWords];          // stream words, byte-swapped, reverse word order
   uint32_t out_w[kOutCap / 4 + 4];  // output staging (global layout, zero-filled)
-  uint2 rec[kT + 1];                // per boundary: (input byte index, output byte index)
-  uint32_t olen[kT];                // out_len | status << 31
-  uint16_t order[kT];               // literals by ascending encoded length
+  uint2 rec[kL + 1];                // per boundary: (input byte index, output byte index)
+  uint32_t olen[kL];                // out_len | status << 31
+  uint16_t order[kL];               // literals by ascending encoded length
   uint32_t hist[kBuckets];
   uint64_t base[2];                 // the sub-tile's in_off / out_off at its first literal
 };
@@ -115,6 +118,7 @@ __device__ void decode_literal_global(const uint8_t *src, uint64_t nbytes, uint8
   *status = st;
 }
 
+#ifdef MHQ_DEC_WINDOW
 // The 32 stream bits at bit position p (one ds_read2_b32 of logical words k, k+1).
 __device__ __forceinline__ uint32_t window_at(const uint32_t *in_w, uint32_t p) {
   const uint32_t k = p >> 5, sh = p & 31u;
@@ -122,6 +126,7 @@ __device__ __forceinline__ uint32_t window_at(const uint32_t *in_w, uint32_t p) 
   const uint64_t ww = (uint64_t)wp[0] | ((uint64_t)wp[1] << 32);  // {word k+1, word k}
   return (uint32_t)((ww << sh) >> 32);
 }
+#endif
 
 // Decodes staged literal bits [p, endbit) into staging bytes [optr, oend).
 // Returns out_len | status << 31.
@@ -131,14 +136,29 @@ __device__ __forceinline__ uint32_t decode_one(Smem &sm, uint32_t p, uint32_t en
   uint32_t acc = 0;  // this literal's bytes of word optr>>2 below optr
   uint32_t bad = 0;
   bool fin = false;
+#ifndef MHQ_DEC_WINDOW
+  // 64-bit bit buffer: the next nb >= 32 stream bits, MSB first.  The refill
+  // word is read ahead of each probe, so a probe waits on one LDS round trip
+  // (its LUT entry) instead of two.
+  uint32_t rem = endbit - p;
+  uint32_t nxt = (p >> 5) + 2u;  // logical index of the next word to load
+  uint64_t bb = ((uint64_t)sm.in_w[kInWords - 1u - (p >> 5)] << 32 | sm.in_w[kInWords - 2u - (p >> 5)])
+                << (p & 31u);
+  uint32_t nb = 64u - (p & 31u);
+#endif
   while (!fin) {
     const uint32_t w0 = optr >> 2;
     uint64_t o64 = acc;
 #pragma unroll
     for (int u = 0; u < 2; u++) {  // two probes per output flush
+#ifdef MHQ_DEC_WINDOW
       const uint32_t win = window_at(sm.in_w, p);
-      const uint32_t e = sm.lut1[win >> (32 - kLut1Bits)];
       const uint32_t rem = endbit - p;
+#else
+      const uint32_t win = (uint32_t)(bb >> 32);
+      const uint32_t wnext = sm.in_w[kInWords - 1u - nxt];
+#endif
+      const uint32_t e = sm.lut1[win >> (32 - kLut1Bits)];
       uint32_t len0 = (e >> 16) & 31u, tot = (e >> 21) & 31u, ns = e >> 26, syms = e & 0xffffu;
       if (ns == 0) {  // a code of 13..30 bits, or the all-ones EOS prefix
         const uint32_t nw = ~win;
@@ -160,7 +180,19 @@ __device__ __forceinline__ uint32_t decode_one(Smem &sm, uint32_t p, uint32_t en
       cnt = fin ? 0u : cnt;
       o64 |= (uint64_t)__builtin_amdgcn_ubfe(syms, 0, cnt * 8u) << ((optr - 4u * w0) * 8u);
       optr += cnt;
-      p += cnt ? (ct ? tot : len0) : 0u;
+      const uint32_t used = cnt ? (ct ? tot : len0) : 0u;
+#ifdef MHQ_DEC_WINDOW
+      p += used;
+#else
+      rem -= used;
+      bb <<= used;
+      nb -= used;
+      if (nb < 32u) {  // nb >= 2 here: a probe consumes at most 30 bits
+        bb |= (uint64_t)wnext << (32u - nb);
+        nb += 32u;
+        nxt++;
+      }
+#endif
       fin |= cnt == 0;
     }
     if (o64) {
@@ -186,20 +218,29 @@ __global__ __launch_bounds__(kT) void decode_kernel(
   for (uint32_t i = tid; i < kLut2Size / 8; i += kT) ((u32x4 *)sm.lut2)[i] = ((const u32x4 *)g_lut2)[i];
 
   for (uint64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
-    const uint64_t s = t * kT;
-    const uint32_t cnt = (uint32_t)min((uint64_t)kT, n - s);
-    // the end boundary of literal `tid` (one coalesced u64 each)
-    const uint64_t ie = tid < cnt ? in_off[s + tid + 1] : 0;
-    const uint64_t oe = tid < cnt ? out_off[s + tid + 1] : 0;
+    const uint64_t s = t * kL;
+    const uint32_t cnt = (uint32_t)min((uint64_t)kL, n - s);
+    // end boundaries of literals tid + kT*j (coalesced u64 loads)
+    uint64_t ie[kLPT], oe[kLPT];
+#pragma unroll
+    for (int j = 0; j < kLPT; j++) {
+      const uint32_t l = tid + kT * j;
+      ie[j] = l < cnt ? in_off[s + l + 1] : 0;
+      oe[j] = l < cnt ? out_off[s + l + 1] : 0;
+    }
     uint32_t cur = 0;
     while (cur < cnt) {
       __syncthreads();  // the previous sub-tile is fully consumed
       if (cur == 0 && tid == 0) {
         sm.base[0] = in_off[s];
         sm.base[1] = out_off[s];
-      } else if (cur != 0 && tid == cur - 1) {
-        sm.base[0] = ie;
-        sm.base[1] = oe;
+      }
+#pragma unroll
+      for (int j = 0; j < kLPT; j++) {
+        if (cur != 0 && tid + kT * j == cur - 1) {
+          sm.base[0] = ie[j];
+          sm.base[1] = oe[j];
+        }
       }
       __syncthreads();
       const uint64_t ic = sm.base[0], oc = sm.base[1];
@@ -207,10 +248,17 @@ __global__ __launch_bounds__(kT) void decode_kernel(
       uint8_t *oa = out + (oc - out_bias);
       const uint32_t idelta = (uint32_t)((uintptr_t)ia & 15u);
       const uint32_t odelta = (uint32_t)((uintptr_t)oa & 15u);
-      // literal tid joins the sub-tile when both slices hold everything up to its end
-      const bool fits = tid < cnt && tid >= cur && (ie - ic) + idelta <= (uint64_t)kInCap &&
-                        (oe - oc) + odelta <= (uint64_t)kOutCap;
-      const uint32_t end = cur + (uint32_t)__syncthreads_count(fits);
+      // a literal joins the sub-tile when both slices hold everything up to its end
+      bool fits[kLPT];
+      uint32_t nfit = 0;
+#pragma unroll
+      for (int j = 0; j < kLPT; j++) {
+        const uint32_t l = tid + kT * j;
+        fits[j] = l < cnt && l >= cur && (ie[j] - ic) + idelta <= (uint64_t)kInCap &&
+                  (oe[j] - oc) + odelta <= (uint64_t)kOutCap;
+        nfit += (uint32_t)__syncthreads_count(fits[j]);
+      }
+      const uint32_t end = cur + nfit;
       if (end == cur) {  // one literal larger than the slices
         if (tid == 0)
           decode_literal_global(ia, in_off[s + cur + 1] - ic, oa, out_off[s + cur + 1] - oc, sm.lut1, sm.lut2,
@@ -220,7 +268,11 @@ __global__ __launch_bounds__(kT) void decode_kernel(
       }
       const uint32_t m = end - cur;
       if (tid == 0) sm.rec[0] = make_uint2(idelta, odelta);
-      if (fits) sm.rec[tid - cur + 1] = make_uint2((uint32_t)(ie - ic) + idelta, (uint32_t)(oe - oc) + odelta);
+#pragma unroll
+      for (int j = 0; j < kLPT; j++)
+        if (fits[j])
+          sm.rec[tid + kT * j - cur + 1] =
+              make_uint2((uint32_t)(ie[j] - ic) + idelta, (uint32_t)(oe[j] - oc) + odelta);
       if (tid < kBuckets) sm.hist[tid] = 0;
       __syncthreads();
       const uint32_t in_bytes = sm.rec[m].x, out_bytes = sm.rec[m].y;
@@ -239,12 +291,18 @@ __global__ __launch_bounds__(kT) void decode_kernel(
         const uint32_t ochunks = (out_bytes + 15u) >> 4;
         for (uint32_t c = tid; c < ochunks; c += kT) *(u32x4 *)(sm.out_w + 4u * c) = u32x4{0u, 0u, 0u, 0u};
       }
-      // counting sort by encoded length: the thread of rank r decodes literal order[r]
-      uint32_t bk = 0, rk = 0;
-      if (tid < m) {
-        const uint32_t bytes = sm.rec[tid + 1].x - sm.rec[tid].x;
-        bk = bytes < 32u ? bytes : min(32u + ((bytes - 32u) >> 4), (uint32_t)kBuckets - 1u);
-        rk = atomicAdd(&sm.hist[bk], 1u);
+      // counting sort by encoded length
+      uint32_t bk[kLPT], rk[kLPT];
+#pragma unroll
+      for (int j = 0; j < kLPT; j++) {
+        const uint32_t l = tid + kT * j;
+        bk[j] = 0;
+        rk[j] = 0;
+        if (l < m) {
+          const uint32_t bytes = sm.rec[l + 1].x - sm.rec[l].x;
+          bk[j] = bytes < 32u ? bytes : min(32u + ((bytes - 32u) >> 4), (uint32_t)kBuckets - 1u);
+          rk[j] = atomicAdd(&sm.hist[bk[j]], 1u);
+        }
       }
       __syncthreads();
       if (wave == 0) {  // exclusive scan of the bucket counts
@@ -258,23 +316,36 @@ __global__ __launch_bounds__(kT) void decode_kernel(
         sm.hist[lane] = x - h;
       }
       __syncthreads();
-      if (tid < m) sm.order[sm.hist[bk] + rk] = (uint16_t)tid;
+#pragma unroll
+      for (int j = 0; j < kLPT; j++)
+        if (tid + kT * j < m) sm.order[sm.hist[bk[j]] + rk[j]] = (uint16_t)(tid + kT * j);
       __syncthreads();
-      if (tid < m) {
-        const uint32_t lit = sm.order[tid];
-        const uint2 r0 = sm.rec[lit], r1 = sm.rec[lit + 1];
+      // thread t decodes the literals of rank t and (with two per thread) m-1-t:
+      // short + long pairs, so every lane's work is about the same
+#pragma unroll
+      for (int j = 0; j < kLPT; j++) {
+        const uint32_t r = j == 0 ? tid : m - 1u - tid;
+        const bool mine = kLPT == 1 ? tid < m : (j == 0 ? tid < (m + 1u) / 2u : tid < m / 2u);
+        if (mine) {
+          const uint32_t lit = sm.order[r];
+          const uint2 r0 = sm.rec[lit], r1 = sm.rec[lit + 1];
 #ifdef MHQ_DIAG_NO_DECODE  // diagnostic build: staging and stores only
-        sm.olen[lit] = 0;
+          sm.olen[lit] = 0;
 #else
-        sm.olen[lit] = decode_one(sm, r0.x * 8u, r1.x * 8u, r0.y, r1.y);
+          sm.olen[lit] = decode_one(sm, r0.x * 8u, r1.x * 8u, r0.y, r1.y);
 #endif
+        }
       }
       __syncthreads();
       store_out(oa - odelta, (const uint8_t *)sm.out_w, odelta, out_bytes, tid, kT);
-      if (tid < m) {
-        const uint32_t v = sm.olen[tid];
-        out_len[s + cur + tid] = v & 0x7fffffffu;
-        status[s + cur + tid] = (uint8_t)(v >> 31);
+#pragma unroll
+      for (int j = 0; j < kLPT; j++) {
+        const uint32_t l = tid + kT * j;
+        if (l < m) {
+          const uint32_t v = sm.olen[l];
+          out_len[s + cur + l] = v & 0x7fffffffu;
+          status[s + cur + l] = (uint8_t)(v >> 31);
+        }
       }
       cur = end;
     }
@@ -287,7 +358,7 @@ hipError_t launch_decode(const DevTables &t, const uint8_t *in, const uint64_t *
                          uint64_t n, uint8_t *out, const uint64_t *out_off, uint64_t out_bias,
                          uint32_t *out_len, uint8_t *status, hipStream_t s) {
   if (n == 0) return hipSuccess;
-  const uint64_t ntiles = (n + kT - 1) / kT;
+  const uint64_t ntiles = (n + kL - 1) / kL;
   decode_kernel<<<dim3(dev::tile_grid(ntiles, 1, MHQ_DEC_BLOCKS * MHQ_PER_CU)), dim3(kT), 0, s>>>(
       in, in_off, in_bias, n, out, out_off, out_bias, out_len, status, t.lut1, t.lut2, ntiles);
   return hipGetLastError();
