@@ -94,7 +94,7 @@ int mhq_huff_decode(mhq_ctx *ctx, const uint8_t *in, const uint64_t *in_off, uin
 int mhq_huff_encode_len_dev(mhq_ctx *ctx, int dev, const uint8_t *in, const uint64_t *in_off, uint64_t n,
                             uint32_t *enc_len, void *stream);
 /* out_off[i] = base + sum_{j<i} enc_len[j] (n+1 entries) and, if cap_off is
- * not NULL, cap_off[i] = cap_base + sum_{j<i} floor(8*enc_len[j]/5): the
+ * not NULL, cap_off[i] = base + sum_{j<i} floor(8*enc_len[j]/5): the
  * encode output offsets and the matching decode capacities. */
 int mhq_huff_offsets_dev(mhq_ctx *ctx, int dev, const uint32_t *enc_len, uint64_t n, uint64_t base,
                          uint64_t *out_off, uint64_t *cap_off, void *stream);

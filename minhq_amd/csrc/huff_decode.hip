@@ -34,10 +34,13 @@
 #include "huff_kernels.h"
 #include "huff_table.h"
 
-#ifndef MHQ_DEC_T  // threads per block, literals per thread, and the staging slices
-#define MHQ_DEC_T 384
-#define MHQ_DEC_LPT 2
+#ifndef MHQ_DEC_T  // threads per block
+#define MHQ_DEC_T 768
+#endif
+#ifndef MHQ_DEC_INCAP  // staging slices (bytes)
 #define MHQ_DEC_INCAP 20480
+#endif
+#ifndef MHQ_DEC_OUTCAP
 #define MHQ_DEC_OUTCAP 30720
 #endif
 #ifndef MHQ_DEC_BLOCKS  // resident workgroups per CU
@@ -50,11 +53,15 @@ namespace {
 using namespace dev;
 
 constexpr int kT = MHQ_DEC_T;
-constexpr int kLPT = MHQ_DEC_LPT;  // 1 or 2
-constexpr int kL = kT * kLPT;      // literals per block tile
 constexpr int kInCap = MHQ_DEC_INCAP;    // staged input bytes (incl. 16-B alignment slack)
 constexpr int kOutCap = MHQ_DEC_OUTCAP;  // staged output bytes
 constexpr uint32_t kInWords = kInCap / 4 + 4;
+constexpr int kPF = (kInCap / 16 + kT - 1) / kT;  // prefetched input chunks per thread
+#ifdef MHQ_DEC_PF  // also prefetch the next tile's input into registers (measured: no gain)
+constexpr bool kPrefetchInput = true;
+#else
+constexpr bool kPrefetchInput = false;  // offsets only
+#endif
 constexpr int kBuckets = 64;
 
 struct Smem {
@@ -62,9 +69,9 @@ struct Smem {
   uint16_t lut2[kLut2Size];
   uint32_t in_w[kInWords];          // stream words, byte-swapped, reverse word order
   uint32_t out_w[kOutCap / 4 + 4];  // output staging (global layout, zero-filled)
-  uint2 rec[kL + 1];                // per boundary: (input byte index, output byte index)
-  uint32_t olen[kL];                // out_len | status << 31
-  uint16_t order[kL];               // literals by ascending encoded length
+  uint2 rec[kT + 1];                // per boundary: (input byte index, output byte index)
+  uint32_t olen[kT];                // out_len | status << 31
+  uint16_t order[kT];               // literals by ascending encoded length
   uint32_t hist[kBuckets];
   uint64_t base[2];                 // the sub-tile's in_off / out_off at its first literal
 };
@@ -118,7 +125,6 @@ __device__ void decode_literal_global(const uint8_t *src, uint64_t nbytes, uint8
   *status = st;
 }
 
-#ifdef MHQ_DEC_WINDOW
 // The 32 stream bits at bit position p (one ds_read2_b32 of logical words k, k+1).
 __device__ __forceinline__ uint32_t window_at(const uint32_t *in_w, uint32_t p) {
   const uint32_t k = p >> 5, sh = p & 31u;
@@ -126,52 +132,76 @@ __device__ __forceinline__ uint32_t window_at(const uint32_t *in_w, uint32_t p) 
   const uint64_t ww = (uint64_t)wp[0] | ((uint64_t)wp[1] << 32);  // {word k+1, word k}
   return (uint32_t)((ww << sh) >> 32);
 }
-#endif
+
+// A code of 13..30 bits, or the all-ones EOS prefix (c >= 30): its symbol and
+// length, length 0 for the EOS prefix.
+__device__ __forceinline__ uint32_t long_code(const Smem &sm, uint32_t win, uint32_t &sym) {
+  const uint32_t nw = ~win;
+  const uint32_t c = nw ? (uint32_t)__builtin_clz(nw) : 32u;
+  if (c >= (uint32_t)kEosOnes) return 0;
+  const uint32_t e2 = sm.lut2[(c << kLut2SubBits) | ((win << (c + 1)) >> (32 - kLut2SubBits))];
+  sym = e2 & 0xffu;
+  return e2 >> 8;
+}
 
 // Decodes staged literal bits [p, endbit) into staging bytes [optr, oend).
 // Returns out_len | status << 31.
+//
+// Fast loop: while at least 62 bits remain, two probes (each <= 30 bits) read
+// windows that lie wholly inside the literal, and when the output region can
+// hold floor(bits/5) bytes (the most any input can produce) no probe needs a
+// room or end check: every probe emits its one or two symbols (LUT1 keeps the
+// second symbol 0 for one-symbol entries, so OR-ing 16 bits is exact).  The
+// last bits, and literals with a truncating output region, take the checked
+// loop.  A probe that meets 30 ones before the end here is always INVALID:
+// more than 30 bits remain and the output is not full.
 __device__ __forceinline__ uint32_t decode_one(Smem &sm, uint32_t p, uint32_t endbit, uint32_t optr,
                                                uint32_t oend) {
   const uint32_t ostart = optr;
   uint32_t acc = 0;  // this literal's bytes of word optr>>2 below optr
   uint32_t bad = 0;
+  const bool roomy = oend - optr >= (endbit - p) / 5u;
+  while (roomy && endbit - p >= 62u) {
+    const uint32_t w0 = optr >> 2;
+    uint64_t o64 = acc;
+#pragma unroll
+    for (int u = 0; u < 2; u++) {
+      const uint32_t win = window_at(sm.in_w, p);
+      const uint32_t e = sm.lut1[win >> (32 - kLut1Bits)];
+      uint32_t ns = e >> 26, tot = (e >> 21) & 31u, syms = e & 0xffffu;
+      if (ns == 0) {
+        tot = long_code(sm, win, syms);
+        ns = 1;
+        bad |= tot == 0;
+      }
+      if (!bad) {
+        o64 |= (uint64_t)syms << ((optr - 4u * w0) * 8u);
+        optr += ns;
+        p += tot;
+      }
+    }
+    if (o64) {
+      atomicOr(&sm.out_w[w0], (uint32_t)o64);
+      atomicOr(&sm.out_w[w0 + 1], (uint32_t)(o64 >> 32));
+    }
+    acc = (optr >> 2) != w0 ? (uint32_t)(o64 >> 32) : (uint32_t)o64;
+    if (bad) return (optr - ostart) | (1u << 31);
+  }
   bool fin = false;
-#ifndef MHQ_DEC_WINDOW
-  // 64-bit bit buffer: the next nb >= 32 stream bits, MSB first.  The refill
-  // word is read ahead of each probe, so a probe waits on one LDS round trip
-  // (its LUT entry) instead of two.
-  uint32_t rem = endbit - p;
-  uint32_t nxt = (p >> 5) + 2u;  // logical index of the next word to load
-  uint64_t bb = ((uint64_t)sm.in_w[kInWords - 1u - (p >> 5)] << 32 | sm.in_w[kInWords - 2u - (p >> 5)])
-                << (p & 31u);
-  uint32_t nb = 64u - (p & 31u);
-#endif
   while (!fin) {
     const uint32_t w0 = optr >> 2;
     uint64_t o64 = acc;
 #pragma unroll
     for (int u = 0; u < 2; u++) {  // two probes per output flush
-#ifdef MHQ_DEC_WINDOW
       const uint32_t win = window_at(sm.in_w, p);
       const uint32_t rem = endbit - p;
-#else
-      const uint32_t win = (uint32_t)(bb >> 32);
-      const uint32_t wnext = sm.in_w[kInWords - 1u - nxt];
-#endif
       const uint32_t e = sm.lut1[win >> (32 - kLut1Bits)];
       uint32_t len0 = (e >> 16) & 31u, tot = (e >> 21) & 31u, ns = e >> 26, syms = e & 0xffffu;
-      if (ns == 0) {  // a code of 13..30 bits, or the all-ones EOS prefix
-        const uint32_t nw = ~win;
-        const uint32_t c = nw ? (uint32_t)__builtin_clz(nw) : 32u;
-        if (c >= (uint32_t)kEosOnes) {
-          len0 = tot = 0xffffffffu;         // never fits: the literal ends here
-          bad |= rem > (uint32_t)kEosOnes;  // a 31st bit exists: nil child
-        } else {
-          const uint32_t e2 = sm.lut2[(c << kLut2SubBits) | ((win << (c + 1)) >> (32 - kLut2SubBits))];
-          len0 = tot = (e2 >> 8) ? (e2 >> 8) : 0xffffffffu;
-          ns = 1;
-          syms = e2 & 0xffu;
-        }
+      if (ns == 0) {
+        const uint32_t L = long_code(sm, win, syms);
+        len0 = tot = L ? L : 0xffffffffu;  // the EOS prefix never fits: the literal ends here
+        ns = 1;
+        bad |= L == 0 && rem > (uint32_t)kEosOnes;  // a 31st bit exists: nil child
       }
       const bool ct = tot <= rem;
       uint32_t cnt = ct ? ns : (len0 <= rem ? 1u : 0u);
@@ -180,19 +210,7 @@ __device__ __forceinline__ uint32_t decode_one(Smem &sm, uint32_t p, uint32_t en
       cnt = fin ? 0u : cnt;
       o64 |= (uint64_t)__builtin_amdgcn_ubfe(syms, 0, cnt * 8u) << ((optr - 4u * w0) * 8u);
       optr += cnt;
-      const uint32_t used = cnt ? (ct ? tot : len0) : 0u;
-#ifdef MHQ_DEC_WINDOW
-      p += used;
-#else
-      rem -= used;
-      bb <<= used;
-      nb -= used;
-      if (nb < 32u) {  // nb >= 2 here: a probe consumes at most 30 bits
-        bb |= (uint64_t)wnext << (32u - nb);
-        nb += 32u;
-        nxt++;
-      }
-#endif
+      p += cnt ? (ct ? tot : len0) : 0u;
       fin |= cnt == 0;
     }
     if (o64) {
@@ -205,7 +223,71 @@ __device__ __forceinline__ uint32_t decode_one(Smem &sm, uint32_t p, uint32_t en
   return (optr - ostart) | (bad << 31);
 }
 
-__global__ __launch_bounds__(kT) void decode_kernel(
+#ifdef MHQ_DIAG_STAMPS  // diagnostic build: shader cycles per phase, summed over waves
+__device__ unsigned long long g_diag[8];
+#define STAMP(i)                                                \
+  do {                                                          \
+    const unsigned long long _t = __builtin_amdgcn_s_memtime(); \
+    ph[i] += _t - t_last;                                       \
+    t_last = _t;                                                \
+  } while (0)
+#else
+#define STAMP(i) \
+  do {           \
+  } while (0)
+#endif
+
+// The next tile's offsets and the first kInCap bytes of its input, loaded into
+// registers while the current tile decodes (software pipelining across tiles).
+struct Prefetch {
+  uint64_t i0, o0;  // in_off / out_off at the tile's first literal (uniform)
+  uint32_t ie, oe;  // end boundaries of literal tid, relative to i0 / o0
+  u32x4 v[kPF];     // input chunks tid + kT*k from the tile's 16-B aligned start
+};
+
+__device__ __forceinline__ void tile_bounds(const uint64_t *__restrict__ in_off, uint64_t n, uint64_t t,
+                                            uint64_t ntiles, uint64_t &b0, uint64_t &b1) {
+  b0 = b1 = 0;
+  if (t < ntiles) {
+    const uint64_t s = t * kT;
+    b0 = in_off[s];
+    b1 = in_off[min(s + kT, n)];
+  }
+}
+
+__device__ __forceinline__ void issue_prefetch(Prefetch &pf, const uint8_t *__restrict__ in, uint64_t in_bias,
+                                               const uint64_t *__restrict__ in_off,
+                                               const uint64_t *__restrict__ out_off, uint64_t n, uint64_t t,
+                                               uint64_t ntiles, uint64_t b0, uint64_t b1, uint32_t tid) {
+  if (t >= ntiles) return;
+  const uint64_t s = t * kT;
+  const uint32_t cnt = (uint32_t)min((uint64_t)kT, n - s);
+  pf.i0 = b0;
+  pf.o0 = out_off[s];
+  pf.ie = tid < cnt ? (uint32_t)(in_off[s + tid + 1] - b0) : 0u;
+  pf.oe = tid < cnt ? (uint32_t)(out_off[s + tid + 1] - pf.o0) : 0u;
+  const uint8_t *a = in + (b0 - in_bias);
+  const uint32_t delta = (uint32_t)((uintptr_t)a & 15u);
+  const uint64_t bytes = (b1 - b0) + delta;
+  const uint32_t chunks = (uint32_t)min((bytes + 15u) >> 4, (uint64_t)(kInCap / 16));
+  const u32x4 *src = (const u32x4 *)(a - delta);
+  if (!kPrefetchInput) return;
+#pragma unroll
+  for (int k = 0; k < kPF; k++) {
+    const uint32_t c = tid + (uint32_t)kT * k;
+    if (c < chunks) pf.v[k] = __builtin_nontemporal_load(src + c);  // aligned: never crosses a page
+  }
+}
+
+__device__ __forceinline__ void put_in_chunk(Smem &sm, uint32_t c, u32x4 v) {
+  v.x = __builtin_bswap32(v.x);
+  v.y = __builtin_bswap32(v.y);
+  v.z = __builtin_bswap32(v.z);
+  v.w = __builtin_bswap32(v.w);
+  *(u32x4 *)(sm.in_w + kInWords - 4u - 4u * c) = v.wzyx;
+}
+
+__global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(kT / 256 * MHQ_DEC_BLOCKS))) void decode_kernel(
     const uint8_t *__restrict__ in, const uint64_t *__restrict__ in_off, uint64_t in_bias, uint64_t n,
     uint8_t *__restrict__ out, const uint64_t *__restrict__ out_off, uint64_t out_bias,
     uint32_t *__restrict__ out_len, uint8_t *__restrict__ status, const uint32_t *__restrict__ g_lut1,
@@ -214,95 +296,98 @@ __global__ __launch_bounds__(kT) void decode_kernel(
   const uint32_t tid = threadIdx.x;
   const uint32_t lane = tid % kWave;
   const uint32_t wave = tid / kWave;
+  const uint64_t G = gridDim.x;
+  uint64_t t = blockIdx.x;
+  Prefetch pf;
+  uint64_t b0, b1;
+  tile_bounds(in_off, n, t, ntiles, b0, b1);
+  issue_prefetch(pf, in, in_bias, in_off, out_off, n, t, ntiles, b0, b1, tid);
+  tile_bounds(in_off, n, t + G, ntiles, b0, b1);  // bounds of the block's next tile
   for (uint32_t i = tid; i < kLut1Size / 4; i += kT) ((u32x4 *)sm.lut1)[i] = ((const u32x4 *)g_lut1)[i];
   for (uint32_t i = tid; i < kLut2Size / 8; i += kT) ((u32x4 *)sm.lut2)[i] = ((const u32x4 *)g_lut2)[i];
+#ifdef MHQ_DIAG_STAMPS
+  unsigned long long ph[7] = {0, 0, 0, 0, 0, 0, 0};
+  unsigned long long t_last = __builtin_amdgcn_s_memtime();
+#endif
 
-  for (uint64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
-    const uint64_t s = t * kL;
-    const uint32_t cnt = (uint32_t)min((uint64_t)kL, n - s);
-    // end boundaries of literals tid + kT*j (coalesced u64 loads)
-    uint64_t ie[kLPT], oe[kLPT];
-#pragma unroll
-    for (int j = 0; j < kLPT; j++) {
-      const uint32_t l = tid + kT * j;
-      ie[j] = l < cnt ? in_off[s + l + 1] : 0;
-      oe[j] = l < cnt ? out_off[s + l + 1] : 0;
-    }
+  for (; t < ntiles; t += G) {
+    const uint64_t s = t * kT;
+    const uint32_t cnt = (uint32_t)min((uint64_t)kT, n - s);
+    const uint32_t ie = pf.ie, oe = pf.oe;  // end boundary of literal tid, relative to i0 / o0
+    const uint64_t i0 = pf.i0, o0 = pf.o0;
+    bool first = true;  // pf.v holds the start of this tile's input
     uint32_t cur = 0;
     while (cur < cnt) {
       __syncthreads();  // the previous sub-tile is fully consumed
-      if (cur == 0 && tid == 0) {
-        sm.base[0] = in_off[s];
-        sm.base[1] = out_off[s];
-      }
-#pragma unroll
-      for (int j = 0; j < kLPT; j++) {
-        if (cur != 0 && tid + kT * j == cur - 1) {
-          sm.base[0] = ie[j];
-          sm.base[1] = oe[j];
-        }
+      if (cur != 0 && tid == cur - 1) {
+        sm.base[0] = ie;
+        sm.base[1] = oe;
       }
       __syncthreads();
-      const uint64_t ic = sm.base[0], oc = sm.base[1];
-      const uint8_t *ia = in + (ic - in_bias);
-      uint8_t *oa = out + (oc - out_bias);
+      // sub-tile start, relative to the tile's start
+      const uint32_t ic = cur == 0 ? 0u : (uint32_t)sm.base[0], oc = cur == 0 ? 0u : (uint32_t)sm.base[1];
+      const uint8_t *ia = in + (i0 + ic - in_bias);
+      uint8_t *oa = out + (o0 + oc - out_bias);
       const uint32_t idelta = (uint32_t)((uintptr_t)ia & 15u);
       const uint32_t odelta = (uint32_t)((uintptr_t)oa & 15u);
-      // a literal joins the sub-tile when both slices hold everything up to its end
-      bool fits[kLPT];
-      uint32_t nfit = 0;
-#pragma unroll
-      for (int j = 0; j < kLPT; j++) {
-        const uint32_t l = tid + kT * j;
-        fits[j] = l < cnt && l >= cur && (ie[j] - ic) + idelta <= (uint64_t)kInCap &&
-                  (oe[j] - oc) + odelta <= (uint64_t)kOutCap;
-        nfit += (uint32_t)__syncthreads_count(fits[j]);
-      }
-      const uint32_t end = cur + nfit;
+      // literal tid joins the sub-tile when both slices hold everything up to its end
+      const bool fits = tid < cnt && tid >= cur && (ie - ic) + idelta <= (uint32_t)kInCap &&
+                        (oe - oc) + odelta <= (uint32_t)kOutCap;
+      const uint32_t end = cur + (uint32_t)__syncthreads_count(fits);
+      STAMP(0);
       if (end == cur) {  // one literal larger than the slices
+        if (first) {
+          issue_prefetch(pf, in, in_bias, in_off, out_off, n, t + G, ntiles, b0, b1, tid);
+          tile_bounds(in_off, n, t + 2 * G, ntiles, b0, b1);
+          first = false;
+        }
         if (tid == 0)
-          decode_literal_global(ia, in_off[s + cur + 1] - ic, oa, out_off[s + cur + 1] - oc, sm.lut1, sm.lut2,
+          decode_literal_global(ia, in_off[s + cur + 1] - (i0 + ic), oa, out_off[s + cur + 1] - (o0 + oc), sm.lut1, sm.lut2,
                                 out_len + s + cur, status + s + cur);
         cur++;
         continue;
       }
       const uint32_t m = end - cur;
       if (tid == 0) sm.rec[0] = make_uint2(idelta, odelta);
-#pragma unroll
-      for (int j = 0; j < kLPT; j++)
-        if (fits[j])
-          sm.rec[tid + kT * j - cur + 1] =
-              make_uint2((uint32_t)(ie[j] - ic) + idelta, (uint32_t)(oe[j] - oc) + odelta);
+      if (fits) sm.rec[tid - cur + 1] = make_uint2(ie - ic + idelta, oe - oc + odelta);
       if (tid < kBuckets) sm.hist[tid] = 0;
       __syncthreads();
       const uint32_t in_bytes = sm.rec[m].x, out_bytes = sm.rec[m].y;
       // stage the input (byte-swapped, reverse word order); zero the output slice
-      {
-        const uint32_t chunks = (in_bytes + 15u) >> 4;
+      const uint32_t chunks = (in_bytes + 15u) >> 4;
+      if (first) {
         const u32x4 *src = (const u32x4 *)(ia - idelta);
-        for (uint32_t c = tid; c < chunks; c += kT) {
-          u32x4 v = __builtin_nontemporal_load(src + c);  // aligned: never crosses a page
-          v.x = __builtin_bswap32(v.x);
-          v.y = __builtin_bswap32(v.y);
-          v.z = __builtin_bswap32(v.z);
-          v.w = __builtin_bswap32(v.w);
-          *(u32x4 *)(sm.in_w + kInWords - 4u - 4u * c) = v.wzyx;
+#pragma unroll
+        for (int k = 0; k < kPF; k++) {
+          if (!kPrefetchInput) break;
+          const uint32_t c = tid + (uint32_t)kT * k;
+          if (c < chunks) put_in_chunk(sm, c, pf.v[k]);
         }
+        if (!kPrefetchInput)
+          for (uint32_t c = tid; c < chunks; c += kT) put_in_chunk(sm, c, __builtin_nontemporal_load(src + c));
+        // the registers are free again: start loading the block's next tile
+        issue_prefetch(pf, in, in_bias, in_off, out_off, n, t + G, ntiles, b0, b1, tid);
+        tile_bounds(in_off, n, t + 2 * G, ntiles, b0, b1);
+        first = false;
+      } else {
+        const u32x4 *src = (const u32x4 *)(ia - idelta);
+        for (uint32_t c = tid; c < chunks; c += kT) put_in_chunk(sm, c, __builtin_nontemporal_load(src + c));
+      }
+      {
         const uint32_t ochunks = (out_bytes + 15u) >> 4;
         for (uint32_t c = tid; c < ochunks; c += kT) *(u32x4 *)(sm.out_w + 4u * c) = u32x4{0u, 0u, 0u, 0u};
       }
-      // counting sort by encoded length
-      uint32_t bk[kLPT], rk[kLPT];
-#pragma unroll
-      for (int j = 0; j < kLPT; j++) {
-        const uint32_t l = tid + kT * j;
-        bk[j] = 0;
-        rk[j] = 0;
-        if (l < m) {
-          const uint32_t bytes = sm.rec[l + 1].x - sm.rec[l].x;
-          bk[j] = bytes < 32u ? bytes : min(32u + ((bytes - 32u) >> 4), (uint32_t)kBuckets - 1u);
-          rk[j] = atomicAdd(&sm.hist[bk[j]], 1u);
-        }
+      STAMP(1);
+#ifdef MHQ_DEC_NOSORT
+      __syncthreads();
+      const uint32_t lit = tid;
+#else
+      // counting sort by encoded length: the thread of rank r decodes literal order[r]
+      uint32_t bk = 0, rk = 0;
+      if (tid < m) {
+        const uint32_t bytes = sm.rec[tid + 1].x - sm.rec[tid].x;
+        bk = bytes < 32u ? bytes : min(32u + ((bytes - 32u) >> 4), (uint32_t)kBuckets - 1u);
+        rk = atomicAdd(&sm.hist[bk], 1u);
       }
       __syncthreads();
       if (wave == 0) {  // exclusive scan of the bucket counts
@@ -316,49 +401,58 @@ __global__ __launch_bounds__(kT) void decode_kernel(
         sm.hist[lane] = x - h;
       }
       __syncthreads();
-#pragma unroll
-      for (int j = 0; j < kLPT; j++)
-        if (tid + kT * j < m) sm.order[sm.hist[bk[j]] + rk[j]] = (uint16_t)(tid + kT * j);
+      if (tid < m) sm.order[sm.hist[bk] + rk] = (uint16_t)tid;
       __syncthreads();
-      // thread t decodes the literals of rank t and (with two per thread) m-1-t:
-      // short + long pairs, so every lane's work is about the same
-#pragma unroll
-      for (int j = 0; j < kLPT; j++) {
-        const uint32_t r = j == 0 ? tid : m - 1u - tid;
-        const bool mine = kLPT == 1 ? tid < m : (j == 0 ? tid < (m + 1u) / 2u : tid < m / 2u);
-        if (mine) {
-          const uint32_t lit = sm.order[r];
-          const uint2 r0 = sm.rec[lit], r1 = sm.rec[lit + 1];
-#ifdef MHQ_DIAG_NO_DECODE  // diagnostic build: staging and stores only
-          sm.olen[lit] = 0;
-#else
-          sm.olen[lit] = decode_one(sm, r0.x * 8u, r1.x * 8u, r0.y, r1.y);
+      const uint32_t lit = tid < m ? sm.order[tid] : 0u;
 #endif
-        }
+      STAMP(2);
+      if (tid < m) {
+        const uint2 r0 = sm.rec[lit], r1 = sm.rec[lit + 1];
+#ifdef MHQ_DIAG_NO_DECODE  // diagnostic build: staging and stores only
+        sm.olen[lit] = 0;
+#else
+        sm.olen[lit] = decode_one(sm, r0.x * 8u, r1.x * 8u, r0.y, r1.y);
+#endif
       }
+      STAMP(3);
       __syncthreads();
+      STAMP(4);
       store_out(oa - odelta, (const uint8_t *)sm.out_w, odelta, out_bytes, tid, kT);
-#pragma unroll
-      for (int j = 0; j < kLPT; j++) {
-        const uint32_t l = tid + kT * j;
-        if (l < m) {
-          const uint32_t v = sm.olen[l];
-          out_len[s + cur + l] = v & 0x7fffffffu;
-          status[s + cur + l] = (uint8_t)(v >> 31);
-        }
+      if (tid < m) {
+        const uint32_t v = sm.olen[tid];
+        out_len[s + cur + tid] = v & 0x7fffffffu;
+        status[s + cur + tid] = (uint8_t)(v >> 31);
       }
       cur = end;
+      STAMP(5);
+#ifdef MHQ_DIAG_STAMPS
+      ph[6]++;
+#endif
     }
   }
+#ifdef MHQ_DIAG_STAMPS
+  if (lane == 0)
+    for (int i = 0; i < 7; i++) atomicAdd(&g_diag[i], ph[i]);
+#endif
 }
 
 }  // namespace
+
+#ifdef MHQ_DIAG_STAMPS
+extern "C" int mhq_diag_read(unsigned long long *out, int n) {
+  unsigned long long h[8];
+  if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_diag), sizeof(h)) != hipSuccess) return -1;
+  for (int i = 0; i < n && i < 8; i++) out[i] = h[i];
+  unsigned long long z[8] = {0};
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_diag), z, sizeof(z)) == hipSuccess ? 0 : -1;
+}
+#endif
 
 hipError_t launch_decode(const DevTables &t, const uint8_t *in, const uint64_t *in_off, uint64_t in_bias,
                          uint64_t n, uint8_t *out, const uint64_t *out_off, uint64_t out_bias,
                          uint32_t *out_len, uint8_t *status, hipStream_t s) {
   if (n == 0) return hipSuccess;
-  const uint64_t ntiles = (n + kL - 1) / kL;
+  const uint64_t ntiles = (n + kT - 1) / kT;
   decode_kernel<<<dim3(dev::tile_grid(ntiles, 1, MHQ_DEC_BLOCKS * MHQ_PER_CU)), dim3(kT), 0, s>>>(
       in, in_off, in_bias, n, out, out_off, out_bias, out_len, status, t.lut1, t.lut2, ntiles);
   return hipGetLastError();

@@ -120,11 +120,12 @@ def main():
     ms = e0.elapsed_time(e1) / args.iters
     if diag:
         diag(buf, 8)
-        tot = sum(buf[:5]) or 1
+        names = ["offs_fit", "stage", "sort", "decode", "barrier", "store"]
+        tot = sum(buf[:6]) or 1
         print("diag phases (share of wave cycles): " + " ".join(
-            f"{nm}={buf[i] / tot:.3f}" for i, nm in enumerate(["offs_fit", "stage", "split", "decode", "store"])),
-            f"wave-cycles/launch={tot / args.iters:.3g} decode-iters/launch={buf[5] / args.iters:.4g}"
-            f" cycles/iter={buf[3] / max(buf[5], 1):.1f}", file=sys.stderr)
+            f"{nm}={buf[i] / tot:.3f}" for i, nm in enumerate(names)),
+            f"wave-cycles/launch={tot / args.iters:.3g} sub-tiles/launch={buf[6] / args.iters:.4g}"
+            f" decode-cycles/sub-tile/wave={buf[3] / max(buf[6], 1):.1f}", file=sys.stderr)
     if args.kernel == "decode" and not args.no_check:
         s = slots[0]
         assert int(s["st"].sum().item()) == 0
