@@ -5,245 +5,304 @@
 // 1 bits; encode_len is ceil(sum of code lengths / 8), the size the Auto
 // choice compares with the raw length (hc/io.go:172).
 //
-// Structure (one workgroup = kWaves wave64s, the code table in LDS): each
-// wave walks tiles of kTileLits literals staged in its LDS slice.  A tile's
-// bytes are processed in rounds of 1 KiB: lane l takes the 16-byte chunk
-// 64r + l, looks up the 16 codes, and a wave prefix sum of the chunk bit
-// totals places every byte's code in the tile's bit stream (S = running sum
-// of code lengths over the tile).  A literal's bit offset is S minus S at its
-// first byte, so a lane never waits for another lane's bytes: the work is
-// perfectly balanced whatever the literal lengths.  Output words are
-// assembled in registers and OR-ed into the zeroed staging area (words at
-// chunk and literal boundaries are shared), then written back with aligned
-// 16-B stores.
+// Structure: one workgroup of kT threads owns a block tile of kT consecutive
+// literals and encodes it with one thread per literal (the same skeleton as
+// huff_decode.hip):
+//   * the tile's plaintext is staged in LDS (aligned 16-B loads) and read back
+//     a word (4 bytes) at a time; the 256-entry code table sits in LDS too;
+//   * a counting sort by plaintext length gives thread t the literal of rank
+//     t, so the 64 literals of a wave have similar lengths;
+//   * each thread appends codes to a 64-bit bit buffer and writes complete
+//     big-endian words straight to HBM as aligned dword stores; the first and
+//     last words of a literal (shared with its neighbours) go byte by byte;
+//   * while a tile is encoded, the block's next tile's offsets and plaintext
+//     are in flight into registers;
+//   * a tile whose plaintext exceeds the staging slice is processed as several
+//     sub-tiles; a single literal larger than the slice is encoded by one
+//     thread straight from global memory.
 #include <hip/hip_runtime.h>
 
 #include "huff_common.h"
 #include "huff_kernels.h"
 #include "huff_table.h"
 
+#ifndef MHQ_ENC_T  // threads (= literals) per block tile
+#define MHQ_ENC_T 768
+#endif
+#ifndef MHQ_ENC_INCAP  // plaintext staging slice (bytes)
+#define MHQ_ENC_INCAP 36864
+#endif
+#ifndef MHQ_ENC_BLOCKS  // resident workgroups per CU
+#define MHQ_ENC_BLOCKS 2
+#endif
+
 namespace mhq {
 namespace {
 
 using namespace dev;
 
-constexpr int kWaves = 8;
-constexpr int kThreads = kWave * kWaves;
-constexpr int kTileLits = 256;
-constexpr int kInCap = 6144;   // staged input bytes per wave (incl. 16-B alignment slack)
-constexpr int kOutCap = 6144;  // staged output bytes per wave (encode only)
-constexpr int kChunks = kInCap / 16;
+constexpr int kT = MHQ_ENC_T;
+constexpr int kInCap = MHQ_ENC_INCAP;
+constexpr int kPF = (kInCap / 16 + kT - 1) / kT;  // prefetched input chunks per thread
+constexpr int kBuckets = 64;
 
-struct WaveSmem {
-  uint32_t in_w[kInCap / 4];
-  uint32_t out_w[kOutCap / 4 + 4];
-  uint2 rec[kTileLits + 2];   // per boundary: (input byte index, output byte index)
-  uint32_t sstart[kTileLits]; // S at the literal's first byte
-  uint32_t obits[kTileLits];  // encoded bits per literal (encode_len)
-  uint16_t lit_at[kChunks];   // literal holding the first byte of each chunk
-};
 struct Smem {
-  uint2 code[256];  // (code left-aligned in 32 bits, length)
-  WaveSmem w[kWaves];
+  uint2 code[256];                // (code right-justified, length)
+  uint32_t in_w[kInCap / 4 + 4];  // plaintext, natural byte order
+  uint2 rec[kT + 1];              // per boundary: (input byte index in in_w, output offset from the sub-tile start)
+  uint16_t order[kT];             // literals by ascending plaintext length
+  uint32_t hist[kBuckets];
+  uint32_t base[2];  // the sub-tile's start (input, output) relative to the tile
 };
 
-// Appends `len` bits (MSB-aligned in `cla`) at bit position bp of the LDS
-// word stream `ow`; acc holds this lane's bits of word bp>>5 (MSB-aligned in
-// its upper half).  Complete words are OR-ed out.
-__device__ __forceinline__ void put_bits(uint32_t *ow, uint64_t &acc, uint32_t &bp, uint32_t cla, uint32_t len) {
-  const uint32_t sh = bp & 31u;
-  acc |= ((uint64_t)cla << 32) >> sh;
-  if (sh + len >= 32u) {
-    atomicOr(&ow[bp >> 5], __builtin_bswap32((uint32_t)(acc >> 32)));
-    acc <<= 32;
+// Bit writer over global bytes o[ostart, ...): complete words are stored as
+// aligned big-endian dwords, except a first word that starts before ostart
+// (shared with the previous literal), which is stored byte by byte.
+struct BitOut {
+  uint8_t *o;       // 4-byte aligned
+  uint32_t ostart;  // first byte of this literal
+  uint32_t wpos;    // byte position of the word being filled (multiple of 4)
+  uint32_t nbits;   // bits pending in acc (its low nbits bits), counting the junk prefix
+  uint64_t acc;
+
+  __device__ __forceinline__ void init(uint8_t *o_, uint32_t start) {
+    o = o_;
+    ostart = start;
+    wpos = start & ~3u;
+    nbits = (start & 3u) * 8u;  // bytes of the word before the literal: never stored
+    acc = 0;
   }
-  bp += len;
+  __device__ __forceinline__ void store_word(uint32_t w_be) {  // first byte in bits 31..24
+    if (wpos >= ostart) {
+      *(uint32_t *)(o + wpos) = __builtin_bswap32(w_be);
+    } else {
+      for (uint32_t b = ostart - wpos; b < 4u; b++) o[wpos + b] = (uint8_t)(w_be >> (24u - 8u * b));
+    }
+    wpos += 4u;
+  }
+  __device__ __forceinline__ void put(uint32_t code, uint32_t len) {
+    acc = (acc << len) | code;
+    nbits += len;
+    if (nbits >= 32u) {
+      nbits -= 32u;
+      store_word((uint32_t)(acc >> nbits));
+    }
+  }
+  // Pad with 1 bits to an octet boundary (bitWriter.Pad(0xff)) and store the rest.
+  __device__ __forceinline__ void finish() {
+    const uint32_t padn = (8u - (nbits & 7u)) & 7u;
+    acc = (acc << padn) | ((1u << padn) - 1u);
+    nbits += padn;
+    for (uint32_t b = 0; b * 8u < nbits; b++) {
+      const uint32_t x = wpos + b;
+      if (x >= ostart) o[x] = (uint8_t)(acc >> (nbits - 8u * (b + 1u)));
+    }
+  }
+};
+
+// One literal, one thread, straight from global memory (literals larger than
+// the staging slice).
+template <bool kEmit>
+__device__ void encode_literal_global(const uint8_t *src, uint64_t nbytes, uint8_t *dst, const uint2 *code,
+                                      uint32_t *enc_len) {
+  uint64_t bits = 0;
+  BitOut bo;
+  if (kEmit) bo.init((uint8_t *)((uintptr_t)dst & ~(uintptr_t)3), (uint32_t)((uintptr_t)dst & 3u));
+  for (uint64_t i = 0; i < nbytes; i++) {
+    const uint2 c = code[src[i]];
+    bits += c.y;
+    if (kEmit) bo.put(c.x, c.y);
+  }
+  if (kEmit) bo.finish();
+  if (!kEmit) *enc_len = (uint32_t)((bits + 7u) / 8u);
 }
 
-// OR-s out the partial word at bp (if any bits of it are pending).
-__device__ __forceinline__ void put_flush(uint32_t *ow, uint64_t acc, uint32_t bp) {
-  if (bp & 31u) atomicOr(&ow[bp >> 5], __builtin_bswap32((uint32_t)(acc >> 32)));
+// Encodes staged plaintext bytes [p, e); returns the encoded bit count.
+template <bool kEmit>
+__device__ __forceinline__ uint32_t encode_one(const Smem &sm, uint32_t p, uint32_t e, uint8_t *o, uint32_t ostart) {
+  uint32_t bits = 0;
+  BitOut bo;
+  if (kEmit) bo.init(o, ostart);
+  for (uint32_t q = p & ~3u; q < e; q += 4u) {
+    const uint32_t w = sm.in_w[q >> 2];
+#pragma unroll
+    for (int b = 0; b < 4; b++) {
+      const uint32_t x = q + (uint32_t)b;
+      uint2 c = sm.code[(w >> (8 * b)) & 0xffu];
+      if (x < p || x >= e) c = make_uint2(0u, 0u);
+      bits += c.y;
+      if (kEmit) bo.put(c.x, c.y);
+    }
+  }
+  if (kEmit) bo.finish();
+  return bits;
+}
+
+// ---- software pipeline across a block's tiles (as in huff_decode.hip) ----
+
+__device__ __forceinline__ uint32_t vzero() {
+  uint32_t z;
+  asm volatile("v_mov_b32 %0, 0" : "=v"(z));
+  return z;
+}
+
+__device__ __forceinline__ uint64_t vload(const uint64_t *__restrict__ p, uint64_t i) { return p[i + vzero()]; }
+
+__device__ __forceinline__ uint64_t uniform64(uint64_t v) {
+  return (uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)v) |
+         ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32);
+}
+
+struct TileBounds {  // raw: in_off at the tile's first literal and at its end
+  uint64_t b0, b1;
+};
+
+struct TileLoads {      // raw
+  uint64_t o0;          // out_off at the tile's first literal (encode)
+  uint64_t ie64, oe64;  // in_off / out_off at the end of literal min(tid, cnt-1)
+  u32x4 v[kPF];         // plaintext chunk min(tid + kT*k, chunks-1) from the 16-B aligned start
+};
+
+__device__ __forceinline__ TileBounds load_bounds(const uint64_t *__restrict__ in_off, uint64_t n, uint64_t t,
+                                                  uint64_t ntiles) {
+  const uint64_t s = min(t, ntiles - 1u) * kT;
+  return TileBounds{vload(in_off, s), vload(in_off, min(s + kT, n))};
+}
+
+__device__ __forceinline__ uint32_t prefetch_chunks(const uint8_t *in, uint64_t in_bias, uint64_t b0, uint64_t b1) {
+  const uint32_t delta = (uint32_t)((uintptr_t)(in + (b0 - in_bias)) & 15u);
+  return (uint32_t)min(((b1 - b0) + delta + 15u) >> 4, (uint64_t)(kInCap / 16));
 }
 
 template <bool kEmit>
-__global__ __launch_bounds__(kThreads) void encode_kernel(
+__device__ __forceinline__ void issue_tile(TileLoads &tl, const uint8_t *__restrict__ in, uint64_t in_bias,
+                                           const uint64_t *__restrict__ in_off,
+                                           const uint64_t *__restrict__ out_off, uint64_t n, uint64_t t,
+                                           uint64_t ntiles, uint64_t b0, uint64_t b1, uint32_t tid) {
+  const uint64_t s = min(t, ntiles - 1u) * kT;
+  const uint32_t cnt = (uint32_t)min((uint64_t)kT, n - s);
+  const uint64_t j = s + 1u + min(tid, cnt - 1u);
+  tl.ie64 = in_off[j];
+  if (kEmit) {
+    tl.o0 = vload(out_off, s);
+    tl.oe64 = out_off[j];
+  }
+  const uint8_t *a = in + (b0 - in_bias);
+  const u32x4 *src = (const u32x4 *)(a - ((uintptr_t)a & 15u));
+  const uint32_t chunks = prefetch_chunks(in, in_bias, b0, b1);
+#pragma unroll
+  for (int k = 0; k < kPF; k++) {
+    const uint32_t c = min(tid + (uint32_t)kT * k, chunks ? chunks - 1u : 0u);
+    tl.v[k] = __builtin_nontemporal_load(src + c);  // aligned: never crosses a page
+  }
+}
+
+__device__ __forceinline__ void stage_chunks(Smem &sm, const u32x4 *src, uint32_t chunks, uint32_t tid) {
+  u32x4 v[kPF];
+#pragma unroll
+  for (int k = 0; k < kPF; k++) {
+    const uint32_t c = tid + (uint32_t)kT * k;
+    if (c < chunks) v[k] = __builtin_nontemporal_load(src + c);  // aligned: never crosses a page
+  }
+#pragma unroll
+  for (int k = 0; k < kPF; k++) {
+    const uint32_t c = tid + (uint32_t)kT * k;
+    if (c < chunks) *(u32x4 *)(sm.in_w + 4u * c) = v[k];
+  }
+}
+
+template <bool kEmit>
+__global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(kT / 256 * MHQ_ENC_BLOCKS))) void encode_kernel(
     const uint8_t *__restrict__ in, const uint64_t *__restrict__ in_off, uint64_t in_bias, uint64_t n,
     uint8_t *__restrict__ out, const uint64_t *__restrict__ out_off, uint64_t out_bias,
     uint32_t *__restrict__ enc_len, const uint32_t *__restrict__ g_code, const uint8_t *__restrict__ g_len,
     uint64_t ntiles) {
   __shared__ Smem sm;
-  const int tid = threadIdx.x;
-  const int wave = __builtin_amdgcn_readfirstlane(tid / kWave);
-  const int lane = tid % kWave;
-  for (int i = tid; i < 256; i += kThreads) {
-    const uint32_t L = g_len[i];
-    sm.code[i] = make_uint2(g_code[i] << (32u - L), L);
-  }
-  __syncthreads();
-  WaveSmem &ws = sm.w[wave];
-  const uint64_t stride = (uint64_t)gridDim.x * kWaves;
+  const uint32_t tid = threadIdx.x;
+  const uint32_t lane = tid % kWave;
+  const uint32_t wave = tid / kWave;
+  const uint64_t G = gridDim.x;
+  uint64_t t = blockIdx.x;
+  TileBounds cb = load_bounds(in_off, n, t, ntiles);
+  uint64_t b0 = uniform64(cb.b0), b1 = uniform64(cb.b1);
+  TileLoads tl;
+  issue_tile<kEmit>(tl, in, in_bias, in_off, out_off, n, t, ntiles, b0, b1, tid);
+  TileBounds nb = load_bounds(in_off, n, t + G, ntiles);
+  for (uint32_t i = tid; i < 256u; i += kT) sm.code[i] = make_uint2(g_code[i], g_len[i]);
 
-  for (uint64_t t = (uint64_t)blockIdx.x * kWaves + wave; t < ntiles; t += stride) {
-    const uint64_t s = t * kTileLits;
-    const uint32_t cnt = (uint32_t)min((uint64_t)kTileLits, n - s);
-    TileOffsets<kTileLits> off;
-    off.load(in_off, kEmit ? out_off : nullptr, s, cnt, lane);
+  for (; t < ntiles; t += G) {
+    const uint64_t s = t * kT;
+    const uint32_t cnt = (uint32_t)min((uint64_t)kT, n - s);
+    __syncthreads();  // the previous sub-tile is done: in_w is free
+    const uint64_t i0 = b0, o0 = kEmit ? uniform64(tl.o0) : 0u;
+    const uint32_t ie = (uint32_t)(tl.ie64 - i0), oe = kEmit ? (uint32_t)(tl.oe64 - o0) : 0u;
+    {
+      const uint32_t chunks = prefetch_chunks(in, in_bias, b0, b1);
+#pragma unroll
+      for (int k = 0; k < kPF; k++) {
+        const uint32_t c = tid + (uint32_t)kT * k;
+        if (c < chunks) *(u32x4 *)(sm.in_w + 4u * c) = tl.v[k];
+      }
+    }
+    b0 = uniform64(nb.b0);
+    b1 = uniform64(nb.b1);
+    issue_tile<kEmit>(tl, in, in_bias, in_off, out_off, n, t + G, ntiles, b0, b1, tid);
+    nb = load_bounds(in_off, n, t + 2 * G, ntiles);
     uint32_t cur = 0;
     while (cur < cnt) {
-      const uint64_t ic = in_off[s + cur];
-      const uint64_t oc = kEmit ? out_off[s + cur] : 0;
-      const uint8_t *ia = in + (ic - in_bias);
-      uint8_t *oa = kEmit ? out + (oc - out_bias) : nullptr;
-      const uint32_t idelta = (uint32_t)((uintptr_t)ia & 15u);
-      const uint32_t odelta = kEmit ? (uint32_t)((uintptr_t)oa & 15u) : 0u;
-      const uint32_t end = off.fit(cur, cnt, ic, kInCap - idelta, oc, kEmit ? kOutCap - odelta : ~0ull, lane);
-      if (end == cur) {  // one literal larger than the slice: lane 0 walks it in global memory
-        if (lane == 0) {
-          const uint64_t L = in_off[s + cur + 1] - ic;
-          if (kEmit) {
-            const uint64_t cap = out_off[s + cur + 1] - oc;
-            uint64_t acc = 0, o = 0;
-            uint32_t nacc = 0;
-            for (uint64_t i = 0; i < L; i++) {
-              const uint2 cl = sm.code[ia[i]];
-              acc = (acc << cl.y) | (cl.x >> (32u - cl.y));
-              nacc += cl.y;
-              while (nacc >= 8) {
-                nacc -= 8;
-                if (o < cap) oa[o] = (uint8_t)(acc >> nacc);
-                o++;
-              }
-            }
-            if (nacc && o < cap) oa[o] = (uint8_t)((acc << (8 - nacc)) | ((1u << (8 - nacc)) - 1u));
-          } else {
-            uint64_t bits = 0;
-            for (uint64_t i = 0; i < L; i++) bits += sm.code[ia[i]].y;
-            enc_len[s + cur] = (uint32_t)((bits + 7u) >> 3);
-          }
+      if (cur != 0) {
+        if (tid == cur - 1) {
+          sm.base[0] = ie;
+          sm.base[1] = oe;
         }
+        __syncthreads();
+      }
+      const uint32_t ic = cur == 0 ? 0u : sm.base[0], oc = cur == 0 ? 0u : sm.base[1];
+      const uint8_t *ia = in + (i0 + ic - in_bias);
+      uint8_t *oa = kEmit ? out + (o0 + oc - out_bias) : nullptr;
+      const uint32_t idelta = (uint32_t)((uintptr_t)ia & 15u);
+      const uint32_t odelta = kEmit ? (uint32_t)((uintptr_t)oa & 3u) : 0u;
+      const bool fits = tid < cnt && tid >= cur && (ie - ic) + idelta <= (uint32_t)kInCap;
+      const uint32_t end = cur + (uint32_t)__syncthreads_count(fits);
+      if (end == cur) {  // one literal larger than the slice
+        if (tid == 0)
+          encode_literal_global<kEmit>(ia, in_off[s + cur + 1] - (i0 + ic), oa, sm.code, enc_len + s + cur);
         cur++;
         continue;
       }
       const uint32_t m = end - cur;
-#pragma unroll
-      for (int k = 0; k < TileOffsets<kTileLits>::kPer; k++) {
-        const uint32_t j = (uint32_t)lane + (uint32_t)k * kWave;
-        if (j >= cur && j <= end)
-          ws.rec[j - cur] = make_uint2((uint32_t)(off.io[k] - ic) + idelta,
-                                       kEmit ? (uint32_t)(off.oo[k] - oc) + odelta : 0u);
+      if (tid == 0) sm.rec[0] = make_uint2(idelta, odelta);
+      if (fits) sm.rec[tid - cur + 1] = make_uint2(ie - ic + idelta, oe - oc + odelta);
+      if (tid < kBuckets) sm.hist[tid] = 0;
+      __syncthreads();
+      if (cur != 0) stage_chunks(sm, (const u32x4 *)(ia - idelta), (sm.rec[m].x + 15u) >> 4, tid);
+      // counting sort by plaintext length
+      uint32_t bk = 0, rk = 0;
+      if (tid < m) {
+        const uint32_t bytes = sm.rec[tid + 1].x - sm.rec[tid].x;
+        bk = bytes < 32u ? bytes : min(32u + ((bytes - 32u) >> 4), (uint32_t)kBuckets - 1u);
+        rk = atomicAdd(&sm.hist[bk], 1u);
       }
-      const uint32_t in_bytes = (uint32_t)(in_off[s + end] - ic) + idelta;
-      const uint32_t out_bytes = kEmit ? (uint32_t)(out_off[s + end] - oc) + odelta : 0u;
-      stage_in<false, false>(ws.in_w, 0, ia - idelta, in_bytes, lane);
-      if (kEmit) zero_lds(ws.out_w, out_bytes, lane);
-      for (uint32_t j = lane; j < m; j += kWave) ws.obits[j] = 0;
-      wave_sync();
-      // literal holding the first byte of each chunk
-      for (uint32_t j = lane; j < m; j += kWave) {
-        const uint32_t a = ws.rec[j].x, b = ws.rec[j + 1].x;
-        for (uint32_t c = (a + 15u) >> 4; (c << 4) < b; c++) ws.lit_at[c] = (uint16_t)j;
-      }
-      wave_sync();
-
-      const uint32_t x_lo = ws.rec[0].x, x_hi = ws.rec[m].x;
-      const uint32_t c_lo = x_lo >> 4, c_hi = (x_hi + 15u) >> 4;
-      uint32_t carry = 0;  // S at the start of this round
-      for (uint32_t c0 = c_lo; c0 < c_hi; c0 += kWave) {
-        const uint32_t c = c0 + (uint32_t)lane;
-        const bool live = c < c_hi;
-        const uint32_t x0 = c << 4;
-        u32x4 v = live ? *(const u32x4 *)(ws.in_w + 4u * c) : u32x4{0u, 0u, 0u, 0u};
-        uint32_t lit0 = (live && x0 >= x_lo) ? ws.lit_at[c] : 0u;
-        // pass 1: code lengths of the chunk's bytes
-        uint32_t cla[16], len[16];
-        uint32_t tot = 0;
-#pragma unroll
-        for (int i = 0; i < 16; i++) {
-          const uint32_t x = x0 + (uint32_t)i;
-          const uint32_t byte = (v[i >> 2] >> ((i & 3) * 8)) & 0xffu;
-          const bool in_tile = live && x >= x_lo && x < x_hi;
-          const uint2 cl = sm.code[byte];
-          cla[i] = cl.x;
-          len[i] = in_tile ? cl.y : 0u;
-          tot += len[i];
-        }
-        // exclusive wave scan of chunk totals
-        uint32_t incl = tot;
+      __syncthreads();
+      if (wave == 0) {
+        const uint32_t h = sm.hist[lane];
+        uint32_t x = h;
 #pragma unroll
         for (int d = 1; d < kWave; d <<= 1) {
-          const uint32_t y = __shfl_up(incl, d);
-          if (lane >= d) incl += y;
+          const uint32_t y = __shfl_up(x, d);
+          if ((int)lane >= d) x += y;
         }
-        const uint32_t base = carry + incl - tot;
-        carry += __shfl(incl, kWave - 1);
-        // pass 2a: S at literal starts inside this chunk; encoded bits of literals ending here
-        {
-          uint32_t lit = lit0, sacc = base;
-          uint32_t lo = ws.rec[lit0].x, hi = ws.rec[lit0 + 1].x;  // current literal's byte range
-#pragma unroll
-          for (int i = 0; i < 16; i++) {
-            const uint32_t x = x0 + (uint32_t)i;
-            if (live && x >= x_lo && x < x_hi) {
-              while (x >= hi) {
-                lit++;
-                lo = hi;
-                hi = ws.rec[lit + 1].x;
-              }
-              if (x == lo) ws.sstart[lit] = sacc;
-            }
-            sacc += len[i];
-          }
-        }
-        wave_sync();
-        {
-          uint32_t lit = lit0, sacc = base;
-          uint32_t lo = ws.rec[lit0].x, hi = ws.rec[lit0 + 1].x;  // current literal's byte range
-          uint32_t ss = ws.sstart[lit0];
-          uint64_t acc = 0;
-          uint32_t bp = 0;
-          bool open = false;  // bit buffer positioned in a literal's region
-#pragma unroll
-          for (int i = 0; i < 16; i++) {
-            const uint32_t x = x0 + (uint32_t)i;
-            if (live && x >= x_lo && x < x_hi) {
-              bool moved = false;
-              while (x >= hi) {
-                lit++;
-                lo = hi;
-                hi = ws.rec[lit + 1].x;
-                moved = true;
-              }
-              if (moved) ss = ws.sstart[lit];
-              if (kEmit) {
-                if (!open || x == lo) {
-                  if (open) put_flush(ws.out_w, acc, bp);
-                  acc = 0;
-                  bp = ws.rec[lit].y * 8u + (sacc - ss);
-                  open = true;
-                }
-                put_bits(ws.out_w, acc, bp, cla[i], len[i]);
-              }
-              if (x + 1u == hi) {  // the literal's last byte: Pad(0xff)
-                const uint32_t bits = sacc + len[i] - ss;
-                ws.obits[lit] = bits;
-                if (kEmit) {
-                  const uint32_t pad = (8u - (bp & 7u)) & 7u;
-                  if (pad) put_bits(ws.out_w, acc, bp, 0xffffffffu << (32u - pad), pad);
-                }
-              }
-            }
-            sacc += len[i];
-          }
-          if (kEmit && open) put_flush(ws.out_w, acc, bp);
-        }
-        wave_sync();
+        sm.hist[lane] = x - h;
       }
-      if (kEmit) {
-        store_out(oa - odelta, (const uint8_t *)ws.out_w, odelta, out_bytes, lane);
-      } else {
-        for (uint32_t j = lane; j < m; j += kWave) enc_len[s + cur + j] = (ws.obits[j] + 7u) >> 3;
+      __syncthreads();
+      if (tid < m) sm.order[sm.hist[bk] + rk] = (uint16_t)tid;
+      __syncthreads();
+      if (tid < m) {
+        const uint32_t lit = sm.order[tid];
+        const uint2 r0 = sm.rec[lit], r1 = sm.rec[lit + 1];
+        const uint32_t bits = encode_one<kEmit>(sm, r0.x, r1.x, kEmit ? oa - odelta : nullptr, r0.y);
+        if (!kEmit) enc_len[s + cur + lit] = (bits + 7u) >> 3;
       }
-      wave_sync();
       cur = end;
     }
   }
@@ -254,8 +313,8 @@ __global__ __launch_bounds__(kThreads) void encode_kernel(
 hipError_t launch_encode_len(const DevTables &t, const uint8_t *in, const uint64_t *in_off, uint64_t in_bias,
                              uint64_t n, uint32_t *enc_len, hipStream_t s) {
   if (n == 0) return hipSuccess;
-  const uint64_t ntiles = (n + kTileLits - 1) / kTileLits;
-  encode_kernel<false><<<dim3(dev::tile_grid(ntiles, kWaves, MHQ_PER_CU)), dim3(kThreads), 0, s>>>(
+  const uint64_t ntiles = (n + kT - 1) / kT;
+  encode_kernel<false><<<dim3(dev::tile_grid(ntiles, 1, MHQ_ENC_BLOCKS * MHQ_PER_CU)), dim3(kT), 0, s>>>(
       in, in_off, in_bias, n, nullptr, nullptr, 0, enc_len, t.code, t.len, ntiles);
   return hipGetLastError();
 }
@@ -263,8 +322,8 @@ hipError_t launch_encode_len(const DevTables &t, const uint8_t *in, const uint64
 hipError_t launch_encode(const DevTables &t, const uint8_t *in, const uint64_t *in_off, uint64_t in_bias,
                          uint64_t n, uint8_t *out, const uint64_t *out_off, uint64_t out_bias, hipStream_t s) {
   if (n == 0) return hipSuccess;
-  const uint64_t ntiles = (n + kTileLits - 1) / kTileLits;
-  encode_kernel<true><<<dim3(dev::tile_grid(ntiles, kWaves, MHQ_PER_CU)), dim3(kThreads), 0, s>>>(
+  const uint64_t ntiles = (n + kT - 1) / kT;
+  encode_kernel<true><<<dim3(dev::tile_grid(ntiles, 1, MHQ_ENC_BLOCKS * MHQ_PER_CU)), dim3(kT), 0, s>>>(
       in, in_off, in_bias, n, out, out_off, out_bias, nullptr, t.code, t.len, ntiles);
   return hipGetLastError();
 }
