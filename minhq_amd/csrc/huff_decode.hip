@@ -11,22 +11,22 @@
 //
 // Structure: one workgroup of kT threads owns a block tile of kT consecutive
 // literals and decodes it with one thread per literal.
-//   * the decode is a chain of dependent LUT probes per literal, so what sets
-//     the speed is how many literals a CU has in flight; that is bounded by
-//     LDS, so only what the probes read lives there: the tables (18 KiB) and
-//     the tile's input bytes (aligned 16-B loads, byte-swapped, reverse word
-//     order).  Output bytes go from registers straight to HBM: whole words as
-//     aligned dword stores, a literal's partial first/last word byte by byte
-//     (those words are shared with the neighbouring literals);
+//   * staging: the tile's offsets (one coalesced u64 per thread), its input
+//     bytes (aligned 16-B loads, byte-swapped, reverse word order so that the
+//     logical word pair {k+1, k} is one little-endian u64) and its output
+//     region (zero-filled, global layout) live in LDS; the output leaves as
+//     aligned 16-B stores, out_len/status as coalesced stores;
 //   * balance: a counting sort by encoded length gives thread t the literal
 //     of rank t, so the 64 literals of a wave have similar lengths and the
-//     wave's loop runs about as long as its literals;
-//   * pipelining: while a tile decodes, the block's next tile's offsets and
-//     input are in flight into registers (see "software pipeline" below);
+//     wave's loop runs about as long as its average literal;
+//   * occupancy: two workgroups per CU (2 x kT/64 waves) hide the LDS round
+//     trips of the per-literal decode chains;
 //   * a probe reads LUT1 with the next 12 bits (one or two codes of <= 12
-//     bits) or, for longer codes, LUT2 by count of leading ones;
-//   * a tile whose input exceeds the staging slice is processed as several
-//     sub-tiles; a single literal larger than the slice is decoded by one
+//     bits) or, for longer codes, LUT2 by count of leading ones; output bytes
+//     are packed into registers on the LDS word grid and OR-ed into the zeroed
+//     staging words, so literals that share a word need no ordering.
+//   * a tile whose bytes exceed the staging slices is processed as several
+//     sub-tiles; a single literal larger than a slice is decoded by one
 //     thread straight from global memory.
 #include <hip/hip_runtime.h>
 
@@ -34,11 +34,14 @@
 #include "huff_kernels.h"
 #include "huff_table.h"
 
-#ifndef MHQ_DEC_T  // threads (= literals) per block tile
+#ifndef MHQ_DEC_T  // threads per block
 #define MHQ_DEC_T 768
 #endif
-#ifndef MHQ_DEC_INCAP  // input staging slice (bytes)
-#define MHQ_DEC_INCAP 27648
+#ifndef MHQ_DEC_INCAP  // staging slices (bytes)
+#define MHQ_DEC_INCAP 20480
+#endif
+#ifndef MHQ_DEC_OUTCAP
+#define MHQ_DEC_OUTCAP 30720
 #endif
 #ifndef MHQ_DEC_BLOCKS  // resident workgroups per CU
 #define MHQ_DEC_BLOCKS 2
@@ -50,7 +53,8 @@ namespace {
 using namespace dev;
 
 constexpr int kT = MHQ_DEC_T;
-constexpr int kInCap = MHQ_DEC_INCAP;  // staged input bytes (incl. 16-B alignment slack)
+constexpr int kInCap = MHQ_DEC_INCAP;    // staged input bytes (incl. 16-B alignment slack)
+constexpr int kOutCap = MHQ_DEC_OUTCAP;  // staged output bytes
 constexpr uint32_t kInWords = kInCap / 4 + 4;
 constexpr int kPF = (kInCap / 16 + kT - 1) / kT;  // prefetched input chunks per thread
 #ifdef MHQ_DEC_NOPF  // prefetch only the next tile's offsets, stage its input on arrival
@@ -63,15 +67,17 @@ constexpr int kBuckets = 64;
 struct Smem {
   uint32_t lut1[kLut1Size];
   uint16_t lut2[kLut2Size];
-  uint32_t in_w[kInWords];  // stream words, byte-swapped, reverse word order
-  uint2 rec[kT + 1];        // per boundary: (input byte index in in_w, output offset from the sub-tile start)
-  uint16_t order[kT];       // literals by ascending encoded length
+  uint32_t in_w[kInWords];          // stream words, byte-swapped, reverse word order
+  uint32_t out_w[kOutCap / 4 + 4];  // output staging (global layout, zero-filled)
+  uint2 rec[kT + 1];                // per boundary: (input byte index, output byte index)
+  uint32_t olen[kT];                // out_len | status << 31
+  uint16_t order[kT];               // literals by ascending encoded length
   uint32_t hist[kBuckets];
-  uint32_t base[2];  // the sub-tile's start (input, output) relative to the tile
+  uint64_t base[2];                 // the sub-tile's in_off / out_off at its first literal
 };
 
 // One literal, one thread, straight from global memory: literals too large for
-// the staging slice.  Same decision rules as the staged loop.
+// the staging slices.  Same decision rules as the staged loop.
 __device__ void decode_literal_global(const uint8_t *src, uint64_t nbytes, uint8_t *dst, uint64_t cap,
                                       const uint32_t *lut1, const uint16_t *lut2, uint32_t *out_len,
                                       uint8_t *status) {
@@ -119,6 +125,14 @@ __device__ void decode_literal_global(const uint8_t *src, uint64_t nbytes, uint8
   *status = st;
 }
 
+// The 32 stream bits at bit position p (one ds_read2_b32 of logical words k, k+1).
+__device__ __forceinline__ uint32_t window_at(const uint32_t *in_w, uint32_t p) {
+  const uint32_t k = p >> 5, sh = p & 31u;
+  const uint32_t *wp = in_w + (kInWords - 2u - k);
+  const uint64_t ww = (uint64_t)wp[0] | ((uint64_t)wp[1] << 32);  // {word k+1, word k}
+  return (uint32_t)((ww << sh) >> 32);
+}
+
 // A code of 13..30 bits, or the all-ones EOS prefix (c >= 30): its symbol and
 // length, length 0 for the EOS prefix.
 __device__ __forceinline__ uint32_t long_code(const Smem &sm, uint32_t win, uint32_t &sym) {
@@ -130,93 +144,57 @@ __device__ __forceinline__ uint32_t long_code(const Smem &sm, uint32_t win, uint
   return e2 >> 8;
 }
 
-// Writes bytes [lo, hi) of the little-endian word `w` to wp[lo..hi) (0 <= lo <= hi <= 4).
-__device__ __forceinline__ void store_partial(uint8_t *wp, uint32_t w, uint32_t lo, uint32_t hi) {
-  for (uint32_t b = lo; b < hi; b++) wp[b] = (uint8_t)(w >> (8u * b));
-}
-
-// Decodes staged literal bits [p, endbit) into global bytes o[optr, oend)
-// (o 4-byte aligned).  Returns out_len | status << 31.
+// Decodes staged literal bits [p, endbit) into staging bytes [optr, oend).
+// Returns out_len | status << 31.
 //
-// Input: a 64-bit bit buffer `bb` holds the next nb >= 32 stream bits (MSB
-// first), so a probe's window is its high word and costs no LDS read; the
-// next stream word `sp` is loaded one refill ahead, so the refill is register
-// work and the one LDS round trip on a probe's dependency chain is its LUT1
-// read.  Output: bytes gather in `acc` from the word-aligned position wb; a
-// complete word leaves as one dword store, or byte by byte when it is the
-// literal's first word and starts before the literal (shared with the
-// previous literal); the last partial word leaves byte by byte at the end.
-//
-// Fast loop: while at least 62 bits remain, two probes (each <= 30 bits) see
-// only bits of this literal, and when the output region can hold floor(bits/5)
-// bytes (the most any input can produce) no probe needs a room or end check:
-// every probe emits its one or two symbols (LUT1 keeps the second symbol 0 for
-// one-symbol entries, so OR-ing 16 bits is exact).  A probe that meets 30 ones
-// there is INVALID: more than 30 bits remain and the output is not full.
-// The last bits, and literals with a truncating region, take the checked loop.
-__device__ __forceinline__ uint32_t decode_one(const Smem &sm, uint32_t p, uint32_t endbit, uint8_t *o,
-                                               uint32_t optr, uint32_t oend) {
+// Fast loop: while at least 62 bits remain, two probes (each <= 30 bits) read
+// windows that lie wholly inside the literal, and when the output region can
+// hold floor(bits/5) bytes (the most any input can produce) no probe needs a
+// room or end check: every probe emits its one or two symbols (LUT1 keeps the
+// second symbol 0 for one-symbol entries, so OR-ing 16 bits is exact).  The
+// last bits, and literals with a truncating output region, take the checked
+// loop.  A probe that meets 30 ones before the end here is always INVALID:
+// more than 30 bits remain and the output is not full.
+__device__ __forceinline__ uint32_t decode_one(Smem &sm, uint32_t p, uint32_t endbit, uint32_t optr,
+                                               uint32_t oend) {
   const uint32_t ostart = optr;
-  uint32_t rem = endbit - p;
-  const uint32_t k0 = p >> 5;
-  uint64_t bb = (((uint64_t)sm.in_w[kInWords - 1u - k0] << 32) | sm.in_w[kInWords - 2u - k0]) << (p & 31u);
-  uint32_t nb = 64u - (p & 31u);
-  uint32_t nxt = k0 + 3u;                     // logical index of the word after sp
-  uint32_t sp = sm.in_w[kInWords - 3u - k0];  // logical word k0 + 2
-  uint32_t wb = optr & ~3u;                   // acc holds output bytes [wb, optr)
-  uint64_t acc = 0;
+  uint32_t acc = 0;  // this literal's bytes of word optr>>2 below optr
   uint32_t bad = 0;
-
-#define MHQ_CONSUME(used)                                  \
-  do {                                                     \
-    bb <<= (used);                                         \
-    nb -= (used);                                          \
-    rem -= (used);                                         \
-    if (nb < 32u) { /* nb >= 2: a probe uses <= 30 bits */ \
-      bb |= (uint64_t)sp << (32u - nb);                    \
-      nb += 32u;                                           \
-      sp = sm.in_w[kInWords - 1u - nxt];                   \
-      nxt++;                                               \
-    }                                                      \
-  } while (0)
-#define MHQ_EMIT(syms, count)                                  \
-  do {                                                         \
-    acc |= (uint64_t)(syms) << ((optr - wb) * 8u);             \
-    optr += (count);                                           \
-    if (optr - wb >= 4u) {                                     \
-      if (wb >= ostart)                                        \
-        *(uint32_t *)(o + wb) = (uint32_t)acc;                 \
-      else                                                     \
-        store_partial(o + wb, (uint32_t)acc, ostart - wb, 4u); \
-      acc >>= 32;                                              \
-      wb += 4u;                                                \
-    }                                                          \
-  } while (0)
-
-  const bool roomy = oend - optr >= rem / 5u;
-  while (roomy && rem >= 62u) {
+  const bool roomy = oend - optr >= (endbit - p) / 5u;
+  while (roomy && endbit - p >= 62u) {
+    const uint32_t w0 = optr >> 2;
+    uint64_t o64 = acc;
 #pragma unroll
     for (int u = 0; u < 2; u++) {
-      const uint32_t win = (uint32_t)(bb >> 32);
+      const uint32_t win = window_at(sm.in_w, p);
       const uint32_t e = sm.lut1[win >> (32 - kLut1Bits)];
       uint32_t ns = e >> 26, tot = (e >> 21) & 31u, syms = e & 0xffffu;
       if (ns == 0) {
         tot = long_code(sm, win, syms);
         ns = 1;
-        if (tot == 0) {  // 30 ones with more than 30 bits left: nil child
-          bad = 1;
-          break;
-        }
+        bad |= tot == 0;
       }
-      MHQ_EMIT(syms, ns);
-      MHQ_CONSUME(tot);
+      if (!bad) {
+        o64 |= (uint64_t)syms << ((optr - 4u * w0) * 8u);
+        optr += ns;
+        p += tot;
+      }
     }
-    if (bad) break;
+    if (o64) {
+      atomicOr(&sm.out_w[w0], (uint32_t)o64);
+      atomicOr(&sm.out_w[w0 + 1], (uint32_t)(o64 >> 32));
+    }
+    acc = (optr >> 2) != w0 ? (uint32_t)(o64 >> 32) : (uint32_t)o64;
+    if (bad) return (optr - ostart) | (1u << 31);
   }
-  if (!bad) {
-    bool fin = false;
-    while (!fin) {
-      const uint32_t win = (uint32_t)(bb >> 32);
+  bool fin = false;
+  while (!fin) {
+    const uint32_t w0 = optr >> 2;
+    uint64_t o64 = acc;
+#pragma unroll
+    for (int u = 0; u < 2; u++) {  // two probes per output flush
+      const uint32_t win = window_at(sm.in_w, p);
+      const uint32_t rem = endbit - p;
       const uint32_t e = sm.lut1[win >> (32 - kLut1Bits)];
       uint32_t len0 = (e >> 16) & 31u, tot = (e >> 21) & 31u, ns = e >> 26, syms = e & 0xffffu;
       if (ns == 0) {
@@ -229,17 +207,19 @@ __device__ __forceinline__ uint32_t decode_one(const Smem &sm, uint32_t p, uint3
       uint32_t cnt = ct ? ns : (len0 <= rem ? 1u : 0u);
       const uint32_t room = oend - optr;  // Read() stops once p is full (hc/huffman.go:104)
       cnt = cnt < room ? cnt : room;
-      fin = cnt == 0;
-      if (!fin) {
-        MHQ_EMIT(__builtin_amdgcn_ubfe(syms, 0, cnt * 8u), cnt);
-        MHQ_CONSUME(ct ? tot : len0);
-      }
+      cnt = fin ? 0u : cnt;
+      o64 |= (uint64_t)__builtin_amdgcn_ubfe(syms, 0, cnt * 8u) << ((optr - 4u * w0) * 8u);
+      optr += cnt;
+      p += cnt ? (ct ? tot : len0) : 0u;
+      fin |= cnt == 0;
     }
-    bad = optr != oend ? bad : 0u;
+    if (o64) {
+      atomicOr(&sm.out_w[w0], (uint32_t)o64);
+      atomicOr(&sm.out_w[w0 + 1], (uint32_t)(o64 >> 32));
+    }
+    acc = (optr >> 2) != w0 ? (uint32_t)(o64 >> 32) : (uint32_t)o64;
   }
-  if (optr > wb) store_partial(o + wb, (uint32_t)acc, wb >= ostart ? 0u : ostart - wb, optr - wb);
-#undef MHQ_CONSUME
-#undef MHQ_EMIT
+  bad = optr != oend ? bad : 0u;
   return (optr - ostart) | (bad << 31);
 }
 
@@ -252,11 +232,11 @@ __device__ __forceinline__ unsigned long long stamp_now() {
   __builtin_amdgcn_sched_barrier(0);
   return t;
 }
-#define STAMP(i)                               \
-  do {                                         \
-    const unsigned long long _t = stamp_now(); \
-    ph[i] += _t - t_last;                      \
-    t_last = _t;                               \
+#define STAMP(i)                                    \
+  do {                                              \
+    const unsigned long long _t = stamp_now();      \
+    ph[i] += _t - t_last;                           \
+    t_last = _t;                                    \
   } while (0)
 #else
 #define STAMP(i) \
@@ -273,7 +253,11 @@ __device__ __forceinline__ unsigned long long stamp_now() {
 //     them before they are consumed at the top of the next tile;
 //   * loads are unconditional (clamped addresses) and vector loads, counted
 //     by vmcnt -- a scalar load would be counted by lgkmcnt and drained by
-//     every LDS wait.
+//     every LDS wait;
+//   * gfx9 counts stores in vmcnt too, so waiting for a load also waits for
+//     every store issued before it.  A tile's output is therefore stored
+//     only after the next tile's prefetch has been issued (and consumed
+//     data were loaded before the stores that precede their use).
 
 __device__ __forceinline__ uint32_t vzero() {
   uint32_t z;
@@ -355,7 +339,24 @@ __device__ __forceinline__ void stage_chunks(Smem &sm, const u32x4 *src, uint32_
   }
 }
 
-__global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(kT / 256 * MHQ_DEC_BLOCKS))) void decode_kernel(
+// A decoded sub-tile whose output still sits in LDS (out_w, olen).
+struct Pending {
+  uint8_t *o_al;  // 16-B aligned global address of out_w byte 0
+  uint64_t lit0;  // index of its first literal
+  uint32_t lo, hi, m;
+};
+
+__device__ __forceinline__ void flush(const Smem &sm, const Pending &pd, uint32_t *__restrict__ out_len,
+                                      uint8_t *__restrict__ status, uint32_t tid) {
+  store_out(pd.o_al, (const uint8_t *)sm.out_w, pd.lo, pd.hi, tid, kT);
+  if (tid < pd.m) {
+    const uint32_t v = sm.olen[tid];
+    out_len[pd.lit0 + tid] = v & 0x7fffffffu;
+    status[pd.lit0 + tid] = (uint8_t)(v >> 31);
+  }
+}
+
+__global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu((kT / 64 * MHQ_DEC_BLOCKS + 3) / 4))) void decode_kernel(
     const uint8_t *__restrict__ in, const uint64_t *__restrict__ in_off, uint64_t in_bias, uint64_t n,
     uint8_t *__restrict__ out, const uint64_t *__restrict__ out_off, uint64_t out_bias,
     uint32_t *__restrict__ out_len, uint8_t *__restrict__ status, const uint32_t *__restrict__ g_lut1,
@@ -373,13 +374,15 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(kT / 256 * M
   TileBounds nb = load_bounds(in_off, n, t + G, ntiles);  // tile t+G
   for (uint32_t i = tid; i < kLut1Size / 4; i += kT) ((u32x4 *)sm.lut1)[i] = ((const u32x4 *)g_lut1)[i];
   for (uint32_t i = tid; i < kLut2Size / 8; i += kT) ((u32x4 *)sm.lut2)[i] = ((const u32x4 *)g_lut2)[i];
+  Pending pd{nullptr, 0, 0, 0, 0};
+  bool pending = false;
 #ifdef MHQ_DIAG_STAMPS
   unsigned long long ph[7] = {0, 0, 0, 0, 0, 0, 0};
   unsigned long long t_last = stamp_now();
 #endif
 
   for (; t < ntiles; t += G) {
-#ifdef MHQ_DIAG_COMPUTE_ONLY  // diagnostic build: every tile re-decodes the block's first tile
+#ifdef MHQ_DIAG_COMPUTE_ONLY
     const uint64_t s = (uint64_t)blockIdx.x * kT;
 #else
     const uint64_t s = t * kT;
@@ -398,7 +401,7 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(kT / 256 * M
       }
     }
     // and start loading tile t+G
-#ifdef MHQ_DIAG_COMPUTE_ONLY
+#ifdef MHQ_DIAG_COMPUTE_ONLY  // diagnostic build: every tile re-decodes the block's first tile, no stores
     issue_tile(tl, in, in_bias, in_off, out_off, n, blockIdx.x, ntiles, b0, b1, tid);
 #else
     b0 = uniform64(nb.b0);
@@ -416,16 +419,17 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(kT / 256 * M
         __syncthreads();
       }
       // sub-tile start, relative to the tile's start
-      const uint32_t ic = cur == 0 ? 0u : sm.base[0], oc = cur == 0 ? 0u : sm.base[1];
+      const uint32_t ic = cur == 0 ? 0u : (uint32_t)sm.base[0], oc = cur == 0 ? 0u : (uint32_t)sm.base[1];
       const uint8_t *ia = in + (i0 + ic - in_bias);
       uint8_t *oa = out + (o0 + oc - out_bias);
       const uint32_t idelta = (uint32_t)((uintptr_t)ia & 15u);
-      const uint32_t odelta = (uint32_t)((uintptr_t)oa & 3u);
-      // literal tid joins the sub-tile when the slice holds its input
-      const bool fits = tid < cnt && tid >= cur && (ie - ic) + idelta <= (uint32_t)kInCap;
+      const uint32_t odelta = (uint32_t)((uintptr_t)oa & 15u);
+      // literal tid joins the sub-tile when both slices hold everything up to its end
+      const bool fits = tid < cnt && tid >= cur && (ie - ic) + idelta <= (uint32_t)kInCap &&
+                        (oe - oc) + odelta <= (uint32_t)kOutCap;
       const uint32_t end = cur + (uint32_t)__syncthreads_count(fits);
       STAMP(0);
-      if (end == cur) {  // one literal larger than the slice
+      if (end == cur) {  // one literal larger than the slices
         if (tid == 0)
           decode_literal_global(ia, in_off[s + cur + 1] - (i0 + ic), oa, out_off[s + cur + 1] - (o0 + oc),
                                 sm.lut1, sm.lut2, out_len + s + cur, status + s + cur);
@@ -433,12 +437,22 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(kT / 256 * M
         continue;
       }
       const uint32_t m = end - cur;
+#ifndef MHQ_DIAG_COMPUTE_ONLY
+      if (pending) flush(sm, pd, out_len, status, tid);  // the previous sub-tile's output leaves LDS
+#endif
+      pending = false;
       if (tid == 0) sm.rec[0] = make_uint2(idelta, odelta);
       if (fits) sm.rec[tid - cur + 1] = make_uint2(ie - ic + idelta, oe - oc + odelta);
       if (tid < kBuckets) sm.hist[tid] = 0;
       __syncthreads();
-      // stage the input (byte-swapped, reverse word order) unless the prefetch already did
-      if (!kPrefetchInput || cur != 0) stage_chunks(sm, (const u32x4 *)(ia - idelta), (sm.rec[m].x + 15u) >> 4, tid);
+      const uint32_t in_bytes = sm.rec[m].x, out_bytes = sm.rec[m].y;
+      // stage the input (byte-swapped, reverse word order) unless the prefetch
+      // already did; zero the output slice
+      if (!kPrefetchInput || cur != 0) stage_chunks(sm, (const u32x4 *)(ia - idelta), (in_bytes + 15u) >> 4, tid);
+      {
+        const uint32_t ochunks = (out_bytes + 15u) >> 4;
+        for (uint32_t c = tid; c < ochunks; c += kT) *(u32x4 *)(sm.out_w + 4u * c) = u32x4{0u, 0u, 0u, 0u};
+      }
       STAMP(1);
 #ifdef MHQ_DEC_NOSORT
       __syncthreads();
@@ -470,25 +484,25 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(kT / 256 * M
       STAMP(2);
       if (tid < m) {
         const uint2 r0 = sm.rec[lit], r1 = sm.rec[lit + 1];
-#ifdef MHQ_DIAG_NO_DECODE  // diagnostic build: no decode
-        const uint32_t v = 0;
+#ifdef MHQ_DIAG_NO_DECODE  // diagnostic build: staging and stores only
+        sm.olen[lit] = 0;
 #else
-        const uint32_t v = decode_one(sm, r0.x * 8u, r1.x * 8u, oa - odelta, r0.y, r1.y);
-#endif
-#ifndef MHQ_DIAG_COMPUTE_ONLY
-        out_len[s + cur + lit] = v & 0x7fffffffu;
-        status[s + cur + lit] = (uint8_t)(v >> 31);
-#else
-        if (v == 0xffffffffu) out_len[0] = v;  // keep the decode alive
+        sm.olen[lit] = decode_one(sm, r0.x * 8u, r1.x * 8u, r0.y, r1.y);
 #endif
       }
       STAMP(3);
+      __syncthreads();
+      STAMP(4);
+      pd = Pending{oa - odelta, s + cur, odelta, out_bytes, m};
+      pending = true;
       cur = end;
+      STAMP(5);
 #ifdef MHQ_DIAG_STAMPS
       ph[6]++;
 #endif
     }
   }
+  if (pending) flush(sm, pd, out_len, status, tid);
 #ifdef MHQ_DIAG_STAMPS
   if (lane == 0)
     for (int i = 0; i < 7; i++) atomicAdd(&g_diag[i], ph[i]);

@@ -12,9 +12,11 @@
 //     a word (4 bytes) at a time; the 256-entry code table sits in LDS too;
 //   * a counting sort by plaintext length gives thread t the literal of rank
 //     t, so the 64 literals of a wave have similar lengths;
-//   * each thread appends codes to a 64-bit bit buffer and writes complete
-//     big-endian words straight to HBM as aligned dword stores; the first and
-//     last words of a literal (shared with its neighbours) go byte by byte;
+//   * each thread appends codes to a 64-bit bit buffer and ORs complete
+//     big-endian words into a zeroed LDS staging copy of the tile's output
+//     region (words shared with the neighbouring literals need no ordering:
+//     each literal ORs only its own bits); the region then leaves with
+//     aligned 16-B stores, after the next tile's loads have been issued;
 //   * while a tile is encoded, the block's next tile's offsets and plaintext
 //     are in flight into registers;
 //   * a tile whose plaintext exceeds the staging slice is processed as several
@@ -30,7 +32,10 @@
 #define MHQ_ENC_T 768
 #endif
 #ifndef MHQ_ENC_INCAP  // plaintext staging slice (bytes)
-#define MHQ_ENC_INCAP 36864
+#define MHQ_ENC_INCAP 32768
+#endif
+#ifndef MHQ_ENC_OUTCAP  // output staging slice (bytes, encode only)
+#define MHQ_ENC_OUTCAP 28672
 #endif
 #ifndef MHQ_ENC_BLOCKS  // resident workgroups per CU
 #define MHQ_ENC_BLOCKS 2
@@ -43,60 +48,69 @@ using namespace dev;
 
 constexpr int kT = MHQ_ENC_T;
 constexpr int kInCap = MHQ_ENC_INCAP;
+constexpr int kOutCap = MHQ_ENC_OUTCAP;
 constexpr int kPF = (kInCap / 16 + kT - 1) / kT;  // prefetched input chunks per thread
 constexpr int kBuckets = 64;
 
+template <bool kEmit>
 struct Smem {
   uint2 code[256];                // (code right-justified, length)
   uint32_t in_w[kInCap / 4 + 4];  // plaintext, natural byte order
+  uint32_t out_w[kEmit ? kOutCap / 4 + 4 : 4];  // output staging (global layout, zero-filled)
   uint2 rec[kT + 1];              // per boundary: (input byte index in in_w, output offset from the sub-tile start)
   uint16_t order[kT];             // literals by ascending plaintext length
   uint32_t hist[kBuckets];
   uint32_t base[2];  // the sub-tile's start (input, output) relative to the tile
 };
 
-// Bit writer over global bytes o[ostart, ...): complete words are stored as
-// aligned big-endian dwords, except a first word that starts before ostart
-// (shared with the previous literal), which is stored byte by byte.
+// Bit writer into the zeroed LDS staging words ow[]: complete words are OR-ed
+// in big-endian byte order; bits before the literal's first byte are zero, so
+// a word shared with the previous literal takes only this literal's bits.
 struct BitOut {
-  uint8_t *o;       // 4-byte aligned
-  uint32_t ostart;  // first byte of this literal
-  uint32_t wpos;    // byte position of the word being filled (multiple of 4)
-  uint32_t nbits;   // bits pending in acc (its low nbits bits), counting the junk prefix
+  uint32_t *ow;
+  uint32_t wpos;   // index of the word being filled
+  uint32_t nbits;  // bits pending in acc (its low nbits bits), counting the zero prefix
   uint64_t acc;
 
-  __device__ __forceinline__ void init(uint8_t *o_, uint32_t start) {
-    o = o_;
-    ostart = start;
-    wpos = start & ~3u;
-    nbits = (start & 3u) * 8u;  // bytes of the word before the literal: never stored
+  __device__ __forceinline__ void init(uint32_t *ow_, uint32_t start) {
+    ow = ow_;
+    wpos = start >> 2;
+    nbits = (start & 3u) * 8u;
     acc = 0;
-  }
-  __device__ __forceinline__ void store_word(uint32_t w_be) {  // first byte in bits 31..24
-    if (wpos >= ostart) {
-      *(uint32_t *)(o + wpos) = __builtin_bswap32(w_be);
-    } else {
-      for (uint32_t b = ostart - wpos; b < 4u; b++) o[wpos + b] = (uint8_t)(w_be >> (24u - 8u * b));
-    }
-    wpos += 4u;
   }
   __device__ __forceinline__ void put(uint32_t code, uint32_t len) {
     acc = (acc << len) | code;
     nbits += len;
     if (nbits >= 32u) {
       nbits -= 32u;
-      store_word((uint32_t)(acc >> nbits));
+      atomicOr(&ow[wpos++], __builtin_bswap32((uint32_t)(acc >> nbits)));
     }
   }
-  // Pad with 1 bits to an octet boundary (bitWriter.Pad(0xff)) and store the rest.
+  // Pad with 1 bits to an octet boundary (bitWriter.Pad(0xff)) and OR out the rest.
   __device__ __forceinline__ void finish() {
     const uint32_t padn = (8u - (nbits & 7u)) & 7u;
     acc = (acc << padn) | ((1u << padn) - 1u);
     nbits += padn;
-    for (uint32_t b = 0; b * 8u < nbits; b++) {
-      const uint32_t x = wpos + b;
-      if (x >= ostart) o[x] = (uint8_t)(acc >> (nbits - 8u * (b + 1u)));
+    if (nbits) atomicOr(&ow[wpos], __builtin_bswap32((uint32_t)(acc << (32u - nbits))));
+  }
+};
+
+// Bit writer over global bytes (literals encoded straight from global memory):
+// byte by byte.
+struct BitOutGlobal {
+  uint8_t *o;
+  uint32_t nbits;
+  uint64_t acc;
+  __device__ __forceinline__ void put(uint32_t code, uint32_t len) {
+    acc = (acc << len) | code;
+    nbits += len;
+    while (nbits >= 8u) {
+      nbits -= 8u;
+      *o++ = (uint8_t)(acc >> nbits);
     }
+  }
+  __device__ __forceinline__ void finish() {
+    if (nbits) *o = (uint8_t)((acc << (8u - nbits)) | (0xffu >> nbits));
   }
 };
 
@@ -106,8 +120,7 @@ template <bool kEmit>
 __device__ void encode_literal_global(const uint8_t *src, uint64_t nbytes, uint8_t *dst, const uint2 *code,
                                       uint32_t *enc_len) {
   uint64_t bits = 0;
-  BitOut bo;
-  if (kEmit) bo.init((uint8_t *)((uintptr_t)dst & ~(uintptr_t)3), (uint32_t)((uintptr_t)dst & 3u));
+  BitOutGlobal bo{dst, 0, 0};
   for (uint64_t i = 0; i < nbytes; i++) {
     const uint2 c = code[src[i]];
     bits += c.y;
@@ -119,10 +132,10 @@ __device__ void encode_literal_global(const uint8_t *src, uint64_t nbytes, uint8
 
 // Encodes staged plaintext bytes [p, e); returns the encoded bit count.
 template <bool kEmit>
-__device__ __forceinline__ uint32_t encode_one(const Smem &sm, uint32_t p, uint32_t e, uint8_t *o, uint32_t ostart) {
+__device__ __forceinline__ uint32_t encode_one(Smem<kEmit> &sm, uint32_t p, uint32_t e, uint32_t ostart) {
   uint32_t bits = 0;
   BitOut bo;
-  if (kEmit) bo.init(o, ostart);
+  if (kEmit) bo.init(sm.out_w, ostart);
   for (uint32_t q = p & ~3u; q < e; q += 4u) {
     const uint32_t w = sm.in_w[q >> 2];
 #pragma unroll
@@ -197,7 +210,8 @@ __device__ __forceinline__ void issue_tile(TileLoads &tl, const uint8_t *__restr
   }
 }
 
-__device__ __forceinline__ void stage_chunks(Smem &sm, const u32x4 *src, uint32_t chunks, uint32_t tid) {
+template <bool kEmit>
+__device__ __forceinline__ void stage_chunks(Smem<kEmit> &sm, const u32x4 *src, uint32_t chunks, uint32_t tid) {
   u32x4 v[kPF];
 #pragma unroll
   for (int k = 0; k < kPF; k++) {
@@ -212,12 +226,12 @@ __device__ __forceinline__ void stage_chunks(Smem &sm, const u32x4 *src, uint32_
 }
 
 template <bool kEmit>
-__global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(kT / 256 * MHQ_ENC_BLOCKS))) void encode_kernel(
+__global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu((kT / 64 * MHQ_ENC_BLOCKS + 3) / 4))) void encode_kernel(
     const uint8_t *__restrict__ in, const uint64_t *__restrict__ in_off, uint64_t in_bias, uint64_t n,
     uint8_t *__restrict__ out, const uint64_t *__restrict__ out_off, uint64_t out_bias,
     uint32_t *__restrict__ enc_len, const uint32_t *__restrict__ g_code, const uint8_t *__restrict__ g_len,
     uint64_t ntiles) {
-  __shared__ Smem sm;
+  __shared__ Smem<kEmit> sm;
   const uint32_t tid = threadIdx.x;
   const uint32_t lane = tid % kWave;
   const uint32_t wave = tid / kWave;
@@ -229,6 +243,10 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(kT / 256 * M
   issue_tile<kEmit>(tl, in, in_bias, in_off, out_off, n, t, ntiles, b0, b1, tid);
   TileBounds nb = load_bounds(in_off, n, t + G, ntiles);
   for (uint32_t i = tid; i < 256u; i += kT) sm.code[i] = make_uint2(g_code[i], g_len[i]);
+  // the last sub-tile's output, still in LDS: it leaves once the next loads are issued
+  uint8_t *pd_o = nullptr;
+  uint32_t pd_lo = 0, pd_hi = 0;
+  bool pending = false;
 
   for (; t < ntiles; t += G) {
     const uint64_t s = t * kT;
@@ -261,8 +279,9 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(kT / 256 * M
       const uint8_t *ia = in + (i0 + ic - in_bias);
       uint8_t *oa = kEmit ? out + (o0 + oc - out_bias) : nullptr;
       const uint32_t idelta = (uint32_t)((uintptr_t)ia & 15u);
-      const uint32_t odelta = kEmit ? (uint32_t)((uintptr_t)oa & 3u) : 0u;
-      const bool fits = tid < cnt && tid >= cur && (ie - ic) + idelta <= (uint32_t)kInCap;
+      const uint32_t odelta = kEmit ? (uint32_t)((uintptr_t)oa & 15u) : 0u;
+      const bool fits = tid < cnt && tid >= cur && (ie - ic) + idelta <= (uint32_t)kInCap &&
+                        (!kEmit || (oe - oc) + odelta <= (uint32_t)kOutCap);
       const uint32_t end = cur + (uint32_t)__syncthreads_count(fits);
       if (end == cur) {  // one literal larger than the slice
         if (tid == 0)
@@ -271,11 +290,16 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(kT / 256 * M
         continue;
       }
       const uint32_t m = end - cur;
+      if (kEmit && pending) store_out(pd_o, (const uint8_t *)sm.out_w, pd_lo, pd_hi, tid, kT);
+      pending = false;
       if (tid == 0) sm.rec[0] = make_uint2(idelta, odelta);
       if (fits) sm.rec[tid - cur + 1] = make_uint2(ie - ic + idelta, oe - oc + odelta);
       if (tid < kBuckets) sm.hist[tid] = 0;
       __syncthreads();
       if (cur != 0) stage_chunks(sm, (const u32x4 *)(ia - idelta), (sm.rec[m].x + 15u) >> 4, tid);
+      const uint32_t out_bytes = kEmit ? sm.rec[m].y : 0u;
+      if (kEmit)
+        for (uint32_t c = tid; c < (out_bytes + 15u) >> 4; c += kT) *(u32x4 *)(sm.out_w + 4u * c) = u32x4{0u, 0u, 0u, 0u};
       // counting sort by plaintext length
       uint32_t bk = 0, rk = 0;
       if (tid < m) {
@@ -300,12 +324,20 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(kT / 256 * M
       if (tid < m) {
         const uint32_t lit = sm.order[tid];
         const uint2 r0 = sm.rec[lit], r1 = sm.rec[lit + 1];
-        const uint32_t bits = encode_one<kEmit>(sm, r0.x, r1.x, kEmit ? oa - odelta : nullptr, r0.y);
+        const uint32_t bits = encode_one<kEmit>(sm, r0.x, r1.x, r0.y);
         if (!kEmit) enc_len[s + cur + lit] = (bits + 7u) >> 3;
+      }
+      if (kEmit) {
+        __syncthreads();
+        pd_o = oa - odelta;
+        pd_lo = odelta;
+        pd_hi = out_bytes;
+        pending = true;
       }
       cur = end;
     }
   }
+  if (kEmit && pending) store_out(pd_o, (const uint8_t *)sm.out_w, pd_lo, pd_hi, tid, kT);
 }
 
 }  // namespace

@@ -1,6 +1,5 @@
 // huff_scan.hip -- exclusive scans that turn per-literal lengths into offset
-// arrays (encode output offsets and decode capacities).  Three passes: block
-// sums, one-block scan of the sums, apply.
+// arrays (encode output offsets and decode capacities).
 #include <hip/hip_runtime.h>
 
 #include "huff_common.h"
@@ -27,132 +26,178 @@ int device_cus() {
 
 namespace {
 
+using dev::kWave;
+using dev::u32x4;
+
+// Two passes over n+1 items (item n is 0, so position n receives the total):
+//   1. block sums of (a, b) per chunk of kChunk items;
+//   2. each block adds up the sums of the chunks before it (at most a few
+//      thousand u64 pairs, read from L2), then scans its chunk and writes.
+// A thread owns kItems consecutive items; waves combine with shuffles, the
+// kWaves of a block through LDS.
 constexpr int kScanBlock = 256;
-constexpr int kScanItems = 8;
-constexpr int kScanChunk = kScanBlock * kScanItems;
+constexpr int kItems = 8;
+constexpr int kChunk = kScanBlock * kItems;
+constexpr int kWaves = kScanBlock / kWave;
 
 struct LenVal {  // enc_len -> (bytes, decode capacity)
   const uint32_t *len;
-  __device__ inline void operator()(uint64_t i, uint64_t &a, uint64_t &b) const {
-    const uint64_t v = len[i];
-    a = v;
-    b = (v * 8u) / 5u;
+  uint64_t n;
+  __device__ inline void load(uint64_t i0, uint64_t *a, uint64_t *b) const {
+    uint32_t v[kItems];
+    if (i0 + kItems <= n) {
+      const u32x4 *p = (const u32x4 *)(len + i0);  // i0 is a multiple of kItems: 32-B aligned
+      const u32x4 x = p[0], y = p[1];
+      v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w;
+      v[4] = y.x; v[5] = y.y; v[6] = y.z; v[7] = y.w;
+    } else {
+#pragma unroll
+      for (int k = 0; k < kItems; k++) v[k] = i0 + k < n ? len[i0 + k] : 0u;
+    }
+#pragma unroll
+    for (int k = 0; k < kItems; k++) {
+      a[k] = v[k];
+      b[k] = ((uint64_t)v[k] * 8u) / 5u;
+    }
   }
 };
 struct CapVal {  // in_off -> decode capacity floor(8*len/5)
   const uint64_t *off;
-  __device__ inline void operator()(uint64_t i, uint64_t &a, uint64_t &b) const {
-    const uint64_t v = off[i + 1] - off[i];
-    a = (v * 8u) / 5u;
-    b = 0;
+  uint64_t n;
+  __device__ inline void load(uint64_t i0, uint64_t *a, uint64_t *b) const {
+    uint64_t prev = i0 < n ? off[i0] : 0;
+#pragma unroll
+    for (int k = 0; k < kItems; k++) {
+      const uint64_t i = i0 + k;
+      const uint64_t next = i < n ? off[i + 1] : prev;
+      a[k] = ((next - prev) * 8u) / 5u;
+      b[k] = 0;
+      prev = next;
+    }
   }
 };
 
-__device__ inline void block_scan2(uint64_t &a, uint64_t &b, uint64_t *sa, uint64_t *sb, uint64_t &ta,
-                                   uint64_t &tb) {
-  // inclusive scan of (a,b) across the block; returns block totals
-  const int tid = threadIdx.x;
-  sa[tid] = a;
-  sb[tid] = b;
-  __syncthreads();
-  for (int d = 1; d < kScanBlock; d <<= 1) {
-    uint64_t xa = 0, xb = 0;
-    if (tid >= d) {
-      xa = sa[tid - d];
-      xb = sb[tid - d];
-    }
-    __syncthreads();
-    sa[tid] += xa;
-    sb[tid] += xb;
-    __syncthreads();
+__device__ inline uint64_t wave_sum(uint64_t x) {
+#pragma unroll
+  for (int d = 1; d < kWave; d <<= 1) x += __shfl_xor(x, d);
+  return x;
+}
+
+__device__ inline uint64_t wave_incl_scan(uint64_t x, int lane) {
+#pragma unroll
+  for (int d = 1; d < kWave; d <<= 1) {
+    const uint64_t y = __shfl_up(x, d);
+    if (lane >= d) x += y;
   }
-  a = sa[tid];
-  b = sb[tid];
-  ta = sa[kScanBlock - 1];
-  tb = sb[kScanBlock - 1];
+  return x;
+}
+
+// Block-wide sum of (a, b); every thread gets the result.
+__device__ inline void block_sum2(uint64_t &a, uint64_t &b, uint64_t *sh) {
+  const int tid = threadIdx.x, lane = tid % kWave, wave = tid / kWave;
+  a = wave_sum(a);
+  b = wave_sum(b);
+  if (lane == 0) {
+    sh[2 * wave] = a;
+    sh[2 * wave + 1] = b;
+  }
+  __syncthreads();
+  a = 0;
+  b = 0;
+#pragma unroll
+  for (int w = 0; w < kWaves; w++) {
+    a += sh[2 * w];
+    b += sh[2 * w + 1];
+  }
   __syncthreads();
 }
 
 template <class F>
 __global__ __launch_bounds__(kScanBlock) void scan_reduce_kernel(F f, uint64_t n, uint64_t *sums) {
-  __shared__ uint64_t sa[kScanBlock], sb[kScanBlock];
-  const uint64_t base = (uint64_t)blockIdx.x * kScanChunk + (uint64_t)threadIdx.x * kScanItems;
-  uint64_t a = 0, b = 0;
-  for (int k = 0; k < kScanItems; k++) {
-    if (base + k < n) {
-      uint64_t x, y;
-      f(base + k, x, y);
-      a += x;
-      b += y;
-    }
+  __shared__ uint64_t sh[2 * kWaves];
+  const uint64_t i0 = (uint64_t)blockIdx.x * kChunk + (uint64_t)threadIdx.x * kItems;
+  uint64_t a[kItems], b[kItems];
+  f.load(i0, a, b);
+  uint64_t ta = 0, tb = 0;
+#pragma unroll
+  for (int k = 0; k < kItems; k++) {
+    ta += a[k];
+    tb += b[k];
   }
-  uint64_t ta, tb;
-  block_scan2(a, b, sa, sb, ta, tb);
+  block_sum2(ta, tb, sh);
   if (threadIdx.x == 0) {
     sums[2 * blockIdx.x] = ta;
     sums[2 * blockIdx.x + 1] = tb;
   }
 }
 
-__global__ __launch_bounds__(kScanBlock) void scan_sums_kernel(uint64_t *sums, uint64_t nb) {
-  __shared__ uint64_t sa[kScanBlock], sb[kScanBlock];
-  uint64_t carry_a = 0, carry_b = 0;
-  for (uint64_t base = 0; base < nb; base += kScanBlock) {
-    const uint64_t i = base + threadIdx.x;
-    uint64_t a = i < nb ? sums[2 * i] : 0, b = i < nb ? sums[2 * i + 1] : 0;
-    const uint64_t ea = a, eb = b;
-    uint64_t ta, tb;
-    block_scan2(a, b, sa, sb, ta, tb);
-    if (i < nb) {  // exclusive
-      sums[2 * i] = carry_a + a - ea;
-      sums[2 * i + 1] = carry_b + b - eb;
-    }
-    carry_a += ta;
-    carry_b += tb;
-  }
-}
-
 template <class F>
 __global__ __launch_bounds__(kScanBlock) void scan_apply_kernel(F f, uint64_t n, const uint64_t *sums,
-                                                                 uint64_t base_val, uint64_t *oa,
-                                                                 uint64_t *ob) {
-  __shared__ uint64_t sa[kScanBlock], sb[kScanBlock];
-  const uint64_t base = (uint64_t)blockIdx.x * kScanChunk + (uint64_t)threadIdx.x * kScanItems;
-  uint64_t xa[kScanItems], xb[kScanItems];
-  uint64_t a = 0, b = 0;
-#pragma unroll
-  for (int k = 0; k < kScanItems; k++) {
-    xa[k] = 0;
-    xb[k] = 0;
-    if (base + k < n) f(base + k, xa[k], xb[k]);
-    a += xa[k];
-    b += xb[k];
+                                                                 uint64_t base, uint64_t *oa, uint64_t *ob) {
+  __shared__ uint64_t sh[2 * kWaves];
+  const int tid = threadIdx.x, lane = tid % kWave, wave = tid / kWave;
+  // prefix of the chunks before this one
+  uint64_t pa = 0, pb = 0;
+  for (uint32_t j = tid; j < blockIdx.x; j += kScanBlock) {
+    pa += sums[2 * j];
+    pb += sums[2 * j + 1];
   }
-  const uint64_t la = a, lb = b;
-  uint64_t ta, tb;
-  block_scan2(a, b, sa, sb, ta, tb);
-  uint64_t ra = base_val + sums[2 * blockIdx.x] + a - la;
-  uint64_t rb = base_val + sums[2 * blockIdx.x + 1] + b - lb;
+  block_sum2(pa, pb, sh);
+  // this chunk
+  const uint64_t i0 = (uint64_t)blockIdx.x * kChunk + (uint64_t)tid * kItems;
+  uint64_t a[kItems], b[kItems];
+  f.load(i0, a, b);
+  uint64_t ta = 0, tb = 0;
 #pragma unroll
-  for (int k = 0; k < kScanItems; k++) {
-    if (base + k <= n) {  // position n receives the grand total
-      if (oa) oa[base + k] = ra;
-      if (ob) ob[base + k] = rb;
+  for (int k = 0; k < kItems; k++) {
+    ta += a[k];
+    tb += b[k];
+  }
+  const uint64_t ia = wave_incl_scan(ta, lane), ib = wave_incl_scan(tb, lane);
+  if (lane == kWave - 1) {
+    sh[2 * wave] = ia;
+    sh[2 * wave + 1] = ib;
+  }
+  __syncthreads();
+  uint64_t ra = base + pa + ia - ta, rb = base + pb + ib - tb;
+  for (int w = 0; w < wave; w++) {
+    ra += sh[2 * w];
+    rb += sh[2 * w + 1];
+  }
+  uint64_t xa[kItems], xb[kItems];
+#pragma unroll
+  for (int k = 0; k < kItems; k++) {
+    xa[k] = ra;
+    xb[k] = rb;
+    ra += a[k];
+    rb += b[k];
+  }
+  typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+  if (i0 + kItems <= n + 1) {  // a whole run of outputs: 16-B stores (i0 is a multiple of 8)
+#pragma unroll
+    for (int k = 0; k < kItems; k += 2) {
+      if (oa) *(u64x2 *)(oa + i0 + k) = u64x2{xa[k], xa[k + 1]};
+      if (ob) *(u64x2 *)(ob + i0 + k) = u64x2{xb[k], xb[k + 1]};
     }
-    ra += xa[k];
-    rb += xb[k];
+  } else {
+#pragma unroll
+    for (int k = 0; k < kItems; k++) {
+      if (i0 + k <= n) {
+        if (oa) oa[i0 + k] = xa[k];
+        if (ob) ob[i0 + k] = xb[k];
+      }
+    }
   }
 }
 
 template <class F>
 hipError_t run_scan(F f, uint64_t n, uint64_t base, uint64_t *oa, uint64_t *ob, hipStream_t s) {
   // n+1 outputs; blocks cover indices 0..n inclusive
-  const uint64_t nb = (n + 1 + kScanChunk - 1) / kScanChunk;
+  const uint64_t nb = (n + 1 + kChunk - 1) / kChunk;
   uint64_t *sums = nullptr;
   hipError_t e = hipMallocAsync((void **)&sums, nb * 2 * sizeof(uint64_t), s);
   if (e != hipSuccess) return e;
   scan_reduce_kernel<F><<<dim3((unsigned)nb), dim3(kScanBlock), 0, s>>>(f, n, sums);
-  scan_sums_kernel<<<dim3(1), dim3(kScanBlock), 0, s>>>(sums, nb);
   scan_apply_kernel<F><<<dim3((unsigned)nb), dim3(kScanBlock), 0, s>>>(f, n, sums, base, oa, ob);
   e = hipGetLastError();
   hipError_t e2 = hipFreeAsync(sums, s);
@@ -163,12 +208,12 @@ hipError_t run_scan(F f, uint64_t n, uint64_t base, uint64_t *oa, uint64_t *ob, 
 
 hipError_t launch_offsets(const uint32_t *enc_len, uint64_t n, uint64_t base, uint64_t *out_off,
                           uint64_t *cap_off, hipStream_t s) {
-  return run_scan(LenVal{enc_len}, n, base, out_off, cap_off, s);
+  return run_scan(LenVal{enc_len, n}, n, base, out_off, cap_off, s);
 }
 
 hipError_t launch_capacity(const uint64_t *in_off, uint64_t n, uint64_t base, uint64_t *cap_off,
                            hipStream_t s) {
-  return run_scan(CapVal{in_off}, n, base, cap_off, nullptr, s);
+  return run_scan(CapVal{in_off, n}, n, base, cap_off, nullptr, s);
 }
 
 }  // namespace mhq

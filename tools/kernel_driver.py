@@ -120,7 +120,7 @@ def main():
     ms = e0.elapsed_time(e1) / args.iters
     if diag:
         diag(buf, 8)
-        names = ["offs_fit", "stage", "sort", "decode", "barrier", "store"]
+        names = ["top_fit", "rec_stage", "sort", "decode", "-", "-"]
         tot = sum(buf[:6]) or 1
         print("diag phases (share of wave cycles): " + " ".join(
             f"{nm}={buf[i] / tot:.3f}" for i, nm in enumerate(names)),
