@@ -38,10 +38,10 @@
 #define MHQ_DEC_T 768
 #endif
 #ifndef MHQ_DEC_INCAP  // staging slices (bytes)
-#define MHQ_DEC_INCAP 20480
+#define MHQ_DEC_INCAP 22528
 #endif
 #ifndef MHQ_DEC_OUTCAP
-#define MHQ_DEC_OUTCAP 30720
+#define MHQ_DEC_OUTCAP 34816
 #endif
 #ifndef MHQ_DEC_BLOCKS  // resident workgroups per CU
 #define MHQ_DEC_BLOCKS 2
@@ -69,8 +69,7 @@ struct Smem {
   uint16_t lut2[kLut2Size];
   uint32_t in_w[kInWords];          // stream words, byte-swapped, reverse word order
   uint32_t out_w[kOutCap / 4 + 4];  // output staging (global layout, zero-filled)
-  uint2 rec[kT + 1];                // per boundary: (input byte index, output byte index)
-  uint32_t olen[kT];                // out_len | status << 31
+  uint32_t rec[kT + 1];             // per boundary: input byte index | output byte index << 16
   uint16_t order[kT];               // literals by ascending encoded length
   uint32_t hist[kBuckets];
   uint64_t base[2];                 // the sub-tile's in_off / out_off at its first literal
@@ -339,7 +338,7 @@ __device__ __forceinline__ void stage_chunks(Smem &sm, const u32x4 *src, uint32_
   }
 }
 
-// A decoded sub-tile whose output still sits in LDS (out_w, olen).
+// A decoded sub-tile whose output still sits in LDS (out_w).
 struct Pending {
   uint8_t *o_al;  // 16-B aligned global address of out_w byte 0
   uint64_t lit0;  // index of its first literal
@@ -349,11 +348,6 @@ struct Pending {
 __device__ __forceinline__ void flush(const Smem &sm, const Pending &pd, uint32_t *__restrict__ out_len,
                                       uint8_t *__restrict__ status, uint32_t tid) {
   store_out(pd.o_al, (const uint8_t *)sm.out_w, pd.lo, pd.hi, tid, kT);
-  if (tid < pd.m) {
-    const uint32_t v = sm.olen[tid];
-    out_len[pd.lit0 + tid] = v & 0x7fffffffu;
-    status[pd.lit0 + tid] = (uint8_t)(v >> 31);
-  }
 }
 
 __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu((kT / 64 * MHQ_DEC_BLOCKS + 3) / 4))) void decode_kernel(
@@ -441,11 +435,11 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu((kT / 64 * M
       if (pending) flush(sm, pd, out_len, status, tid);  // the previous sub-tile's output leaves LDS
 #endif
       pending = false;
-      if (tid == 0) sm.rec[0] = make_uint2(idelta, odelta);
-      if (fits) sm.rec[tid - cur + 1] = make_uint2(ie - ic + idelta, oe - oc + odelta);
+      if (tid == 0) sm.rec[0] = idelta | odelta << 16;
+      if (fits) sm.rec[tid - cur + 1] = (ie - ic + idelta) | (oe - oc + odelta) << 16;
       if (tid < kBuckets) sm.hist[tid] = 0;
       __syncthreads();
-      const uint32_t in_bytes = sm.rec[m].x, out_bytes = sm.rec[m].y;
+      const uint32_t in_bytes = sm.rec[m] & 0xffffu, out_bytes = sm.rec[m] >> 16;
       // stage the input (byte-swapped, reverse word order) unless the prefetch
       // already did; zero the output slice
       if (!kPrefetchInput || cur != 0) stage_chunks(sm, (const u32x4 *)(ia - idelta), (in_bytes + 15u) >> 4, tid);
@@ -461,7 +455,7 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu((kT / 64 * M
       // counting sort by encoded length: the thread of rank r decodes literal order[r]
       uint32_t bk = 0, rk = 0;
       if (tid < m) {
-        const uint32_t bytes = sm.rec[tid + 1].x - sm.rec[tid].x;
+        const uint32_t bytes = (sm.rec[tid + 1] & 0xffffu) - (sm.rec[tid] & 0xffffu);
         bk = bytes < 32u ? bytes : min(32u + ((bytes - 32u) >> 4), (uint32_t)kBuckets - 1u);
         rk = atomicAdd(&sm.hist[bk], 1u);
       }
@@ -483,12 +477,14 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu((kT / 64 * M
 #endif
       STAMP(2);
       if (tid < m) {
-        const uint2 r0 = sm.rec[lit], r1 = sm.rec[lit + 1];
+        const uint32_t r0 = sm.rec[lit], r1 = sm.rec[lit + 1];
 #ifdef MHQ_DIAG_NO_DECODE  // diagnostic build: staging and stores only
-        sm.olen[lit] = 0;
+        const uint32_t v = 0;
 #else
-        sm.olen[lit] = decode_one(sm, r0.x * 8u, r1.x * 8u, r0.y, r1.y);
+        const uint32_t v = decode_one(sm, (r0 & 0xffffu) * 8u, (r1 & 0xffffu) * 8u, r0 >> 16, r1 >> 16);
 #endif
+        out_len[s + cur + lit] = v & 0x7fffffffu;
+        status[s + cur + lit] = (uint8_t)(v >> 31);
       }
       STAMP(3);
       __syncthreads();
