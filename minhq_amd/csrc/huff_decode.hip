@@ -72,7 +72,7 @@ struct Smem {
   uint32_t rec[kT + 1];             // per boundary: input byte index | output byte index << 16
   uint16_t order[kT];               // literals by ascending encoded length
   uint32_t hist[kBuckets];
-  uint64_t base[2];                 // the sub-tile's in_off / out_off at its first literal
+  uint64_t nbase[2];                // in_off / out_off at the next sub-tile's first literal
 };
 
 // One literal, one thread, straight from global memory: literals too large for
@@ -243,20 +243,20 @@ __device__ __forceinline__ unsigned long long stamp_now() {
   } while (0)
 #endif
 
-// ---- software pipeline across a block's tiles ----------------------------
-// While tile t decodes, the block's next tile t+G has its offsets and the
-// first kInCap bytes of its input in flight into registers, and the bounds of
-// tile t+2G (which the input prefetch of t+2G needs) too.  Rules that keep
-// the loads asynchronous:
+// ---- a block's literals: one contiguous range, greedy sub-tiles ----------
+// Block b owns literals [b*R, (b+1)*R) (R = ceil(n / grid)).  A sub-tile is
+// the longest run of at most kT literals from `cur` whose input and output
+// fit the staging slices, so tiles stay full whatever the length mix.
+//
+// Software pipeline: as soon as a sub-tile's extent is known, the offsets and
+// the first kInCap input bytes of the next one are issued into registers, so
+// they load while this one decodes.  Rules that keep the loads asynchronous:
 //   * only raw loaded values are kept; no arithmetic, select or copy touches
-//     them before they are consumed at the top of the next tile;
-//   * loads are unconditional (clamped addresses) and vector loads, counted
-//     by vmcnt -- a scalar load would be counted by lgkmcnt and drained by
-//     every LDS wait;
+//     them before they are consumed at the top of the next sub-tile;
+//   * loads are unconditional (clamped addresses);
 //   * gfx9 counts stores in vmcnt too, so waiting for a load also waits for
-//     every store issued before it.  A tile's output is therefore stored
-//     only after the next tile's prefetch has been issued (and consumed
-//     data were loaded before the stores that precede their use).
+//     every store issued before it.  A sub-tile's output is therefore stored
+//     only after the next sub-tile's loads have been issued.
 
 __device__ __forceinline__ uint32_t vzero() {
   uint32_t z;
@@ -271,46 +271,34 @@ __device__ __forceinline__ uint64_t uniform64(uint64_t v) {
          ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32);
 }
 
-struct TileBounds {  // raw: in_off at the tile's first literal and at its end
-  uint64_t b0, b1;
-};
-
-struct TileLoads {      // raw
-  uint64_t o0;          // out_off at the tile's first literal
-  uint64_t ie64, oe64;  // in_off / out_off at the end of literal min(tid, cnt-1)
+struct Next {           // raw loads for the sub-tile that starts at literal `cur`
+  uint64_t ie64, oe64;  // in_off / out_off at the end of literal cur + min(tid, cnt-1)
   u32x4 v[kPF];         // input chunk min(tid + kT*k, chunks-1) from the 16-B aligned start
 };
 
-__device__ __forceinline__ TileBounds load_bounds(const uint64_t *__restrict__ in_off, uint64_t n, uint64_t t,
-                                                  uint64_t ntiles) {
-  const uint64_t s = min(t, ntiles - 1u) * kT;
-  return TileBounds{vload(in_off, s), vload(in_off, min(s + kT, n))};
+// Input chunks the prefetch covers for a sub-tile whose input starts at ic
+// (range input ends at iend).
+__device__ __forceinline__ uint32_t prefetch_chunks(const uint8_t *in, uint64_t in_bias, uint64_t ic, uint64_t iend) {
+  const uint32_t delta = (uint32_t)((uintptr_t)(in + (ic - in_bias)) & 15u);
+  return (uint32_t)min(((iend - ic) + delta + 15u) >> 4, (uint64_t)(kInCap / 16));
 }
 
-__device__ __forceinline__ uint32_t prefetch_chunks(const uint8_t *in, uint64_t in_bias, uint64_t b0, uint64_t b1) {
-  const uint32_t delta = (uint32_t)((uintptr_t)(in + (b0 - in_bias)) & 15u);
-  return (uint32_t)min(((b1 - b0) + delta + 15u) >> 4, (uint64_t)(kInCap / 16));
-}
-
-// b0/b1: the tile's bounds, already uniform.
-__device__ __forceinline__ void issue_tile(TileLoads &tl, const uint8_t *__restrict__ in, uint64_t in_bias,
+// ic: in_off[cur], iend: in_off[lim], both uniform.
+__device__ __forceinline__ void issue_next(Next &nx, const uint8_t *__restrict__ in, uint64_t in_bias,
                                            const uint64_t *__restrict__ in_off,
-                                           const uint64_t *__restrict__ out_off, uint64_t n, uint64_t t,
-                                           uint64_t ntiles, uint64_t b0, uint64_t b1, uint32_t tid) {
-  const uint64_t s = min(t, ntiles - 1u) * kT;
-  const uint32_t cnt = (uint32_t)min((uint64_t)kT, n - s);
-  const uint64_t j = s + 1u + min(tid, cnt - 1u);
-  tl.o0 = vload(out_off, s);
-  tl.ie64 = in_off[j];
-  tl.oe64 = out_off[j];
+                                           const uint64_t *__restrict__ out_off, uint64_t cur, uint64_t lim,
+                                           uint64_t ic, uint64_t iend, uint32_t tid) {
+  const uint64_t j = min(cur + 1u + tid, lim);
+  nx.ie64 = in_off[j];
+  nx.oe64 = out_off[j];
   if (!kPrefetchInput) return;
-  const uint8_t *a = in + (b0 - in_bias);
+  const uint8_t *a = in + (ic - in_bias);
   const u32x4 *src = (const u32x4 *)(a - ((uintptr_t)a & 15u));
-  const uint32_t chunks = prefetch_chunks(in, in_bias, b0, b1);
+  const uint32_t chunks = prefetch_chunks(in, in_bias, ic, iend);
 #pragma unroll
   for (int k = 0; k < kPF; k++) {
     const uint32_t c = min(tid + (uint32_t)kT * k, chunks ? chunks - 1u : 0u);
-    tl.v[k] = __builtin_nontemporal_load(src + c);  // aligned: never crosses a page
+    nx.v[k] = __builtin_nontemporal_load(src + c);  // aligned: never crosses a page
   }
 }
 
@@ -338,115 +326,76 @@ __device__ __forceinline__ void stage_chunks(Smem &sm, const u32x4 *src, uint32_
   }
 }
 
-// A decoded sub-tile whose output still sits in LDS (out_w).
-struct Pending {
-  uint8_t *o_al;  // 16-B aligned global address of out_w byte 0
-  uint64_t lit0;  // index of its first literal
-  uint32_t lo, hi, m;
-};
-
-__device__ __forceinline__ void flush(const Smem &sm, const Pending &pd, uint32_t *__restrict__ out_len,
-                                      uint8_t *__restrict__ status, uint32_t tid) {
-  store_out(pd.o_al, (const uint8_t *)sm.out_w, pd.lo, pd.hi, tid, kT);
-}
-
 __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu((kT / 64 * MHQ_DEC_BLOCKS + 3) / 4))) void decode_kernel(
     const uint8_t *__restrict__ in, const uint64_t *__restrict__ in_off, uint64_t in_bias, uint64_t n,
     uint8_t *__restrict__ out, const uint64_t *__restrict__ out_off, uint64_t out_bias,
     uint32_t *__restrict__ out_len, uint8_t *__restrict__ status, const uint32_t *__restrict__ g_lut1,
-    const uint16_t *__restrict__ g_lut2, uint64_t ntiles) {
+    const uint16_t *__restrict__ g_lut2, uint64_t per_block) {
   __shared__ Smem sm;
   const uint32_t tid = threadIdx.x;
   const uint32_t lane = tid % kWave;
   const uint32_t wave = tid / kWave;
-  const uint64_t G = gridDim.x;
-  uint64_t t = blockIdx.x;
-  TileBounds cb = load_bounds(in_off, n, t, ntiles);  // tile t
-  uint64_t b0 = uniform64(cb.b0), b1 = uniform64(cb.b1);
-  TileLoads tl;
-  issue_tile(tl, in, in_bias, in_off, out_off, n, t, ntiles, b0, b1, tid);
-  TileBounds nb = load_bounds(in_off, n, t + G, ntiles);  // tile t+G
+  const uint64_t L0 = (uint64_t)blockIdx.x * per_block;
+  if (L0 >= n) return;
+  const uint64_t L1 = min(L0 + per_block, n);
+  uint64_t cur = L0;
+  uint64_t i_cur = uniform64(vload(in_off, L0)), o_cur = uniform64(vload(out_off, L0));
+  const uint64_t i_end = uniform64(vload(in_off, L1));
+  Next nx;
+  issue_next(nx, in, in_bias, in_off, out_off, cur, L1, i_cur, i_end, tid);
   for (uint32_t i = tid; i < kLut1Size / 4; i += kT) ((u32x4 *)sm.lut1)[i] = ((const u32x4 *)g_lut1)[i];
   for (uint32_t i = tid; i < kLut2Size / 8; i += kT) ((u32x4 *)sm.lut2)[i] = ((const u32x4 *)g_lut2)[i];
-  Pending pd{nullptr, 0, 0, 0, 0};
+  uint8_t *pd_o = nullptr;  // the previous sub-tile's output, still in LDS
+  uint32_t pd_lo = 0, pd_hi = 0;
   bool pending = false;
 #ifdef MHQ_DIAG_STAMPS
   unsigned long long ph[7] = {0, 0, 0, 0, 0, 0, 0};
   unsigned long long t_last = stamp_now();
 #endif
 
-  for (; t < ntiles; t += G) {
-#ifdef MHQ_DIAG_COMPUTE_ONLY
-    const uint64_t s = (uint64_t)blockIdx.x * kT;
-#else
-    const uint64_t s = t * kT;
-#endif
-    const uint32_t cnt = (uint32_t)min((uint64_t)kT, n - s);
-    __syncthreads();  // the previous sub-tile's decode is done: in_w is free
-    // consume tile t's prefetch
-    const uint64_t i0 = b0, o0 = uniform64(tl.o0);
-    const uint32_t ie = (uint32_t)(tl.ie64 - i0), oe = (uint32_t)(tl.oe64 - o0);  // end of literal tid, tile-relative
-    if (kPrefetchInput) {  // the first kInCap bytes of the tile go to LDS now
-      const uint32_t chunks = prefetch_chunks(in, in_bias, b0, b1);
+  while (cur < L1) {
+    // consume the prefetch (the previous sub-tile's decode ended with a barrier: in_w is free)
+    const uint32_t cnt = (uint32_t)min((uint64_t)kT, L1 - cur);
+    const uint32_t ie = (uint32_t)(nx.ie64 - i_cur), oe = (uint32_t)(nx.oe64 - o_cur);  // end of literal cur+tid
+    const uint8_t *ia = in + (i_cur - in_bias);
+    uint8_t *oa = out + (o_cur - out_bias);
+    const uint32_t idelta = (uint32_t)((uintptr_t)ia & 15u);
+    const uint32_t odelta = (uint32_t)((uintptr_t)oa & 15u);
+    if (kPrefetchInput) {
+      const uint32_t chunks = prefetch_chunks(in, in_bias, i_cur, i_end);
 #pragma unroll
       for (int k = 0; k < kPF; k++) {
         const uint32_t c = tid + (uint32_t)kT * k;
-        if (c < chunks) put_in_chunk(sm, c, tl.v[k]);
+        if (c < chunks) put_in_chunk(sm, c, nx.v[k]);
       }
     }
-    // and start loading tile t+G
-#ifdef MHQ_DIAG_COMPUTE_ONLY  // diagnostic build: every tile re-decodes the block's first tile, no stores
-    issue_tile(tl, in, in_bias, in_off, out_off, n, blockIdx.x, ntiles, b0, b1, tid);
-#else
-    b0 = uniform64(nb.b0);
-    b1 = uniform64(nb.b1);
-    issue_tile(tl, in, in_bias, in_off, out_off, n, t + G, ntiles, b0, b1, tid);
-    nb = load_bounds(in_off, n, t + 2 * G, ntiles);
-#endif
-    uint32_t cur = 0;
-    while (cur < cnt) {
-      if (cur != 0) {
-        if (tid == cur - 1) {
-          sm.base[0] = ie;
-          sm.base[1] = oe;
-        }
-        __syncthreads();
-      }
-      // sub-tile start, relative to the tile's start
-      const uint32_t ic = cur == 0 ? 0u : (uint32_t)sm.base[0], oc = cur == 0 ? 0u : (uint32_t)sm.base[1];
-      const uint8_t *ia = in + (i0 + ic - in_bias);
-      uint8_t *oa = out + (o0 + oc - out_bias);
-      const uint32_t idelta = (uint32_t)((uintptr_t)ia & 15u);
-      const uint32_t odelta = (uint32_t)((uintptr_t)oa & 15u);
-      // literal tid joins the sub-tile when both slices hold everything up to its end
-      const bool fits = tid < cnt && tid >= cur && (ie - ic) + idelta <= (uint32_t)kInCap &&
-                        (oe - oc) + odelta <= (uint32_t)kOutCap;
-      const uint32_t end = cur + (uint32_t)__syncthreads_count(fits);
-      STAMP(0);
-      if (end == cur) {  // one literal larger than the slices
-        if (tid == 0)
-          decode_literal_global(ia, in_off[s + cur + 1] - (i0 + ic), oa, out_off[s + cur + 1] - (o0 + oc),
-                                sm.lut1, sm.lut2, out_len + s + cur, status + s + cur);
-        cur++;
-        continue;
-      }
-      const uint32_t m = end - cur;
-#ifndef MHQ_DIAG_COMPUTE_ONLY
-      if (pending) flush(sm, pd, out_len, status, tid);  // the previous sub-tile's output leaves LDS
-#endif
-      pending = false;
-      if (tid == 0) sm.rec[0] = idelta | odelta << 16;
-      if (fits) sm.rec[tid - cur + 1] = (ie - ic + idelta) | (oe - oc + odelta) << 16;
-      if (tid < kBuckets) sm.hist[tid] = 0;
-      __syncthreads();
+    // the sub-tile: literals cur + [0, m) fit both slices
+    const bool fits = tid < cnt && ie + idelta <= (uint32_t)kInCap && oe + odelta <= (uint32_t)kOutCap;
+    uint32_t m = (uint32_t)__syncthreads_count(fits);
+    const bool oversized = m == 0;  // literal `cur` alone is larger than a slice
+    m = oversized ? 1u : m;
+    STAMP(0);
+    if (tid == m - 1u) {
+      sm.nbase[0] = nx.ie64;
+      sm.nbase[1] = nx.oe64;
+    }
+    if (tid == 0) sm.rec[0] = idelta | odelta << 16;
+    if (fits) sm.rec[tid + 1] = (ie + idelta) | (oe + odelta) << 16;
+    if (tid < kBuckets) sm.hist[tid] = 0;
+    __syncthreads();
+    // start loading the next sub-tile, then let the previous one's output go
+    const uint64_t i_nxt = sm.nbase[0], o_nxt = sm.nbase[1];
+    issue_next(nx, in, in_bias, in_off, out_off, cur + m, L1, i_nxt, i_end, tid);
+    if (pending) store_out(pd_o, (const uint8_t *)sm.out_w, pd_lo, pd_hi, tid, kT);
+    pending = false;
+    if (oversized) {
+      if (tid == 0)
+        decode_literal_global(ia, i_nxt - i_cur, oa, o_nxt - o_cur, sm.lut1, sm.lut2, out_len + cur, status + cur);
+    } else {
       const uint32_t in_bytes = sm.rec[m] & 0xffffu, out_bytes = sm.rec[m] >> 16;
-      // stage the input (byte-swapped, reverse word order) unless the prefetch
-      // already did; zero the output slice
-      if (!kPrefetchInput || cur != 0) stage_chunks(sm, (const u32x4 *)(ia - idelta), (in_bytes + 15u) >> 4, tid);
-      {
-        const uint32_t ochunks = (out_bytes + 15u) >> 4;
-        for (uint32_t c = tid; c < ochunks; c += kT) *(u32x4 *)(sm.out_w + 4u * c) = u32x4{0u, 0u, 0u, 0u};
-      }
+      __syncthreads();  // out_w has been read by the flush
+      if (!kPrefetchInput) stage_chunks(sm, (const u32x4 *)(ia - idelta), (in_bytes + 15u) >> 4, tid);
+      for (uint32_t c = tid; c < (out_bytes + 15u) >> 4; c += kT) *(u32x4 *)(sm.out_w + 4u * c) = u32x4{0u, 0u, 0u, 0u};
       STAMP(1);
 #ifdef MHQ_DEC_NOSORT
       __syncthreads();
@@ -483,22 +432,24 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu((kT / 64 * M
 #else
         const uint32_t v = decode_one(sm, (r0 & 0xffffu) * 8u, (r1 & 0xffffu) * 8u, r0 >> 16, r1 >> 16);
 #endif
-        out_len[s + cur + lit] = v & 0x7fffffffu;
-        status[s + cur + lit] = (uint8_t)(v >> 31);
+        out_len[cur + lit] = v & 0x7fffffffu;
+        status[cur + lit] = (uint8_t)(v >> 31);
       }
       STAMP(3);
-      __syncthreads();
-      STAMP(4);
-      pd = Pending{oa - odelta, s + cur, odelta, out_bytes, m};
+      __syncthreads();  // decode done: in_w free, out_w complete
+      pd_o = oa - odelta;
+      pd_lo = odelta;
+      pd_hi = out_bytes;
       pending = true;
-      cur = end;
-      STAMP(5);
 #ifdef MHQ_DIAG_STAMPS
       ph[6]++;
 #endif
     }
+    cur += m;
+    i_cur = i_nxt;
+    o_cur = o_nxt;
   }
-  if (pending) flush(sm, pd, out_len, status, tid);
+  if (pending) store_out(pd_o, (const uint8_t *)sm.out_w, pd_lo, pd_hi, tid, kT);
 #ifdef MHQ_DIAG_STAMPS
   if (lane == 0)
     for (int i = 0; i < 7; i++) atomicAdd(&g_diag[i], ph[i]);
@@ -521,9 +472,10 @@ hipError_t launch_decode(const DevTables &t, const uint8_t *in, const uint64_t *
                          uint64_t n, uint8_t *out, const uint64_t *out_off, uint64_t out_bias,
                          uint32_t *out_len, uint8_t *status, hipStream_t s) {
   if (n == 0) return hipSuccess;
-  const uint64_t ntiles = (n + kT - 1) / kT;
-  decode_kernel<<<dim3(dev::tile_grid(ntiles, 1, MHQ_DEC_BLOCKS * MHQ_PER_CU)), dim3(kT), 0, s>>>(
-      in, in_off, in_bias, n, out, out_off, out_bias, out_len, status, t.lut1, t.lut2, ntiles);
+  const unsigned grid = dev::tile_grid((n + kT - 1) / kT, 1, MHQ_DEC_BLOCKS * MHQ_PER_CU);
+  const uint64_t per_block = (n + grid - 1) / grid;
+  decode_kernel<<<dim3(grid), dim3(kT), 0, s>>>(in, in_off, in_bias, n, out, out_off, out_bias, out_len, status,
+                                                 t.lut1, t.lut2, per_block);
   return hipGetLastError();
 }
 
