@@ -57,10 +57,10 @@ struct Smem {
   uint2 code[256];                // (code right-justified, length)
   uint32_t in_w[kInCap / 4 + 4];  // plaintext, natural byte order
   uint32_t out_w[kEmit ? kOutCap / 4 + 4 : 4];  // output staging (global layout, zero-filled)
-  uint2 rec[kT + 1];              // per boundary: (input byte index in in_w, output offset from the sub-tile start)
+  uint32_t rec[kT + 1];           // per boundary: input byte index | output byte index << 16
   uint16_t order[kT];             // literals by ascending plaintext length
   uint32_t hist[kBuckets];
-  uint32_t base[2];  // the sub-tile's start (input, output) relative to the tile
+  uint64_t nbase[2];              // in_off / out_off at the next sub-tile's first literal
 };
 
 // Bit writer into the zeroed LDS staging words ow[]: complete words are OR-ed
@@ -151,7 +151,12 @@ __device__ __forceinline__ uint32_t encode_one(Smem<kEmit> &sm, uint32_t p, uint
   return bits;
 }
 
-// ---- software pipeline across a block's tiles (as in huff_decode.hip) ----
+// ---- a block's literals: one contiguous range, greedy sub-tiles ----------
+// As in huff_decode.hip: block b owns literals [b*R, (b+1)*R); a sub-tile is
+// the longest run of at most kT literals that fits the slices; the next
+// sub-tile's offsets and plaintext are loaded into registers while this one
+// is encoded (raw values only, unconditional loads), and a sub-tile's output
+// is stored only after the next sub-tile's loads have been issued.
 
 __device__ __forceinline__ uint32_t vzero() {
   uint32_t z;
@@ -166,62 +171,31 @@ __device__ __forceinline__ uint64_t uniform64(uint64_t v) {
          ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32);
 }
 
-struct TileBounds {  // raw: in_off at the tile's first literal and at its end
-  uint64_t b0, b1;
-};
-
-struct TileLoads {      // raw
-  uint64_t o0;          // out_off at the tile's first literal (encode)
-  uint64_t ie64, oe64;  // in_off / out_off at the end of literal min(tid, cnt-1)
+struct Next {           // raw loads for the sub-tile that starts at literal `cur`
+  uint64_t ie64, oe64;  // in_off / out_off at the end of literal cur + min(tid, cnt-1)
   u32x4 v[kPF];         // plaintext chunk min(tid + kT*k, chunks-1) from the 16-B aligned start
 };
 
-__device__ __forceinline__ TileBounds load_bounds(const uint64_t *__restrict__ in_off, uint64_t n, uint64_t t,
-                                                  uint64_t ntiles) {
-  const uint64_t s = min(t, ntiles - 1u) * kT;
-  return TileBounds{vload(in_off, s), vload(in_off, min(s + kT, n))};
-}
-
-__device__ __forceinline__ uint32_t prefetch_chunks(const uint8_t *in, uint64_t in_bias, uint64_t b0, uint64_t b1) {
-  const uint32_t delta = (uint32_t)((uintptr_t)(in + (b0 - in_bias)) & 15u);
-  return (uint32_t)min(((b1 - b0) + delta + 15u) >> 4, (uint64_t)(kInCap / 16));
+__device__ __forceinline__ uint32_t prefetch_chunks(const uint8_t *in, uint64_t in_bias, uint64_t ic, uint64_t iend) {
+  const uint32_t delta = (uint32_t)((uintptr_t)(in + (ic - in_bias)) & 15u);
+  return (uint32_t)min(((iend - ic) + delta + 15u) >> 4, (uint64_t)(kInCap / 16));
 }
 
 template <bool kEmit>
-__device__ __forceinline__ void issue_tile(TileLoads &tl, const uint8_t *__restrict__ in, uint64_t in_bias,
+__device__ __forceinline__ void issue_next(Next &nx, const uint8_t *__restrict__ in, uint64_t in_bias,
                                            const uint64_t *__restrict__ in_off,
-                                           const uint64_t *__restrict__ out_off, uint64_t n, uint64_t t,
-                                           uint64_t ntiles, uint64_t b0, uint64_t b1, uint32_t tid) {
-  const uint64_t s = min(t, ntiles - 1u) * kT;
-  const uint32_t cnt = (uint32_t)min((uint64_t)kT, n - s);
-  const uint64_t j = s + 1u + min(tid, cnt - 1u);
-  tl.ie64 = in_off[j];
-  if (kEmit) {
-    tl.o0 = vload(out_off, s);
-    tl.oe64 = out_off[j];
-  }
-  const uint8_t *a = in + (b0 - in_bias);
+                                           const uint64_t *__restrict__ out_off, uint64_t cur, uint64_t lim,
+                                           uint64_t ic, uint64_t iend, uint32_t tid) {
+  const uint64_t j = min(cur + 1u + tid, lim);
+  nx.ie64 = in_off[j];
+  if (kEmit) nx.oe64 = out_off[j];
+  const uint8_t *a = in + (ic - in_bias);
   const u32x4 *src = (const u32x4 *)(a - ((uintptr_t)a & 15u));
-  const uint32_t chunks = prefetch_chunks(in, in_bias, b0, b1);
+  const uint32_t chunks = prefetch_chunks(in, in_bias, ic, iend);
 #pragma unroll
   for (int k = 0; k < kPF; k++) {
     const uint32_t c = min(tid + (uint32_t)kT * k, chunks ? chunks - 1u : 0u);
-    tl.v[k] = __builtin_nontemporal_load(src + c);  // aligned: never crosses a page
-  }
-}
-
-template <bool kEmit>
-__device__ __forceinline__ void stage_chunks(Smem<kEmit> &sm, const u32x4 *src, uint32_t chunks, uint32_t tid) {
-  u32x4 v[kPF];
-#pragma unroll
-  for (int k = 0; k < kPF; k++) {
-    const uint32_t c = tid + (uint32_t)kT * k;
-    if (c < chunks) v[k] = __builtin_nontemporal_load(src + c);  // aligned: never crosses a page
-  }
-#pragma unroll
-  for (int k = 0; k < kPF; k++) {
-    const uint32_t c = tid + (uint32_t)kT * k;
-    if (c < chunks) *(u32x4 *)(sm.in_w + 4u * c) = v[k];
+    nx.v[k] = __builtin_nontemporal_load(src + c);  // aligned: never crosses a page
   }
 }
 
@@ -230,80 +204,68 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu((kT / 64 * M
     const uint8_t *__restrict__ in, const uint64_t *__restrict__ in_off, uint64_t in_bias, uint64_t n,
     uint8_t *__restrict__ out, const uint64_t *__restrict__ out_off, uint64_t out_bias,
     uint32_t *__restrict__ enc_len, const uint32_t *__restrict__ g_code, const uint8_t *__restrict__ g_len,
-    uint64_t ntiles) {
+    uint64_t per_block) {
   __shared__ Smem<kEmit> sm;
   const uint32_t tid = threadIdx.x;
   const uint32_t lane = tid % kWave;
   const uint32_t wave = tid / kWave;
-  const uint64_t G = gridDim.x;
-  uint64_t t = blockIdx.x;
-  TileBounds cb = load_bounds(in_off, n, t, ntiles);
-  uint64_t b0 = uniform64(cb.b0), b1 = uniform64(cb.b1);
-  TileLoads tl;
-  issue_tile<kEmit>(tl, in, in_bias, in_off, out_off, n, t, ntiles, b0, b1, tid);
-  TileBounds nb = load_bounds(in_off, n, t + G, ntiles);
+  const uint64_t L0 = (uint64_t)blockIdx.x * per_block;
+  if (L0 >= n) return;
+  const uint64_t L1 = min(L0 + per_block, n);
+  uint64_t cur = L0;
+  uint64_t i_cur = uniform64(vload(in_off, L0)), o_cur = kEmit ? uniform64(vload(out_off, L0)) : 0u;
+  const uint64_t i_end = uniform64(vload(in_off, L1));
+  Next nx;
+  issue_next<kEmit>(nx, in, in_bias, in_off, out_off, cur, L1, i_cur, i_end, tid);
   for (uint32_t i = tid; i < 256u; i += kT) sm.code[i] = make_uint2(g_code[i], g_len[i]);
-  // the last sub-tile's output, still in LDS: it leaves once the next loads are issued
-  uint8_t *pd_o = nullptr;
+  uint8_t *pd_o = nullptr;  // the previous sub-tile's output, still in LDS
   uint32_t pd_lo = 0, pd_hi = 0;
   bool pending = false;
 
-  for (; t < ntiles; t += G) {
-    const uint64_t s = t * kT;
-    const uint32_t cnt = (uint32_t)min((uint64_t)kT, n - s);
-    __syncthreads();  // the previous sub-tile is done: in_w is free
-    const uint64_t i0 = b0, o0 = kEmit ? uniform64(tl.o0) : 0u;
-    const uint32_t ie = (uint32_t)(tl.ie64 - i0), oe = kEmit ? (uint32_t)(tl.oe64 - o0) : 0u;
+  while (cur < L1) {
+    // consume the prefetch (the previous sub-tile ended with a barrier: in_w is free)
+    const uint32_t cnt = (uint32_t)min((uint64_t)kT, L1 - cur);
+    const uint32_t ie = (uint32_t)(nx.ie64 - i_cur), oe = kEmit ? (uint32_t)(nx.oe64 - o_cur) : 0u;
+    const uint8_t *ia = in + (i_cur - in_bias);
+    uint8_t *oa = kEmit ? out + (o_cur - out_bias) : nullptr;
+    const uint32_t idelta = (uint32_t)((uintptr_t)ia & 15u);
+    const uint32_t odelta = kEmit ? (uint32_t)((uintptr_t)oa & 15u) : 0u;
     {
-      const uint32_t chunks = prefetch_chunks(in, in_bias, b0, b1);
+      const uint32_t chunks = prefetch_chunks(in, in_bias, i_cur, i_end);
 #pragma unroll
       for (int k = 0; k < kPF; k++) {
         const uint32_t c = tid + (uint32_t)kT * k;
-        if (c < chunks) *(u32x4 *)(sm.in_w + 4u * c) = tl.v[k];
+        if (c < chunks) *(u32x4 *)(sm.in_w + 4u * c) = nx.v[k];
       }
     }
-    b0 = uniform64(nb.b0);
-    b1 = uniform64(nb.b1);
-    issue_tile<kEmit>(tl, in, in_bias, in_off, out_off, n, t + G, ntiles, b0, b1, tid);
-    nb = load_bounds(in_off, n, t + 2 * G, ntiles);
-    uint32_t cur = 0;
-    while (cur < cnt) {
-      if (cur != 0) {
-        if (tid == cur - 1) {
-          sm.base[0] = ie;
-          sm.base[1] = oe;
-        }
-        __syncthreads();
-      }
-      const uint32_t ic = cur == 0 ? 0u : sm.base[0], oc = cur == 0 ? 0u : sm.base[1];
-      const uint8_t *ia = in + (i0 + ic - in_bias);
-      uint8_t *oa = kEmit ? out + (o0 + oc - out_bias) : nullptr;
-      const uint32_t idelta = (uint32_t)((uintptr_t)ia & 15u);
-      const uint32_t odelta = kEmit ? (uint32_t)((uintptr_t)oa & 15u) : 0u;
-      const bool fits = tid < cnt && tid >= cur && (ie - ic) + idelta <= (uint32_t)kInCap &&
-                        (!kEmit || (oe - oc) + odelta <= (uint32_t)kOutCap);
-      const uint32_t end = cur + (uint32_t)__syncthreads_count(fits);
-      if (end == cur) {  // one literal larger than the slice
-        if (tid == 0)
-          encode_literal_global<kEmit>(ia, in_off[s + cur + 1] - (i0 + ic), oa, sm.code, enc_len + s + cur);
-        cur++;
-        continue;
-      }
-      const uint32_t m = end - cur;
-      if (kEmit && pending) store_out(pd_o, (const uint8_t *)sm.out_w, pd_lo, pd_hi, tid, kT);
-      pending = false;
-      if (tid == 0) sm.rec[0] = make_uint2(idelta, odelta);
-      if (fits) sm.rec[tid - cur + 1] = make_uint2(ie - ic + idelta, oe - oc + odelta);
-      if (tid < kBuckets) sm.hist[tid] = 0;
-      __syncthreads();
-      if (cur != 0) stage_chunks(sm, (const u32x4 *)(ia - idelta), (sm.rec[m].x + 15u) >> 4, tid);
-      const uint32_t out_bytes = kEmit ? sm.rec[m].y : 0u;
-      if (kEmit)
+    const bool fits = tid < cnt && ie + idelta <= (uint32_t)kInCap && (!kEmit || oe + odelta <= (uint32_t)kOutCap);
+    uint32_t m = (uint32_t)__syncthreads_count(fits);
+    const bool oversized = m == 0;  // literal `cur` alone is larger than a slice
+    m = oversized ? 1u : m;
+    if (tid == m - 1u) {
+      sm.nbase[0] = nx.ie64;
+      sm.nbase[1] = kEmit ? nx.oe64 : 0u;
+    }
+    if (tid == 0) sm.rec[0] = idelta | odelta << 16;
+    if (fits) sm.rec[tid + 1] = (ie + idelta) | (oe + odelta) << 16;
+    if (tid < kBuckets) sm.hist[tid] = 0;
+    __syncthreads();
+    const uint64_t i_nxt = sm.nbase[0], o_nxt = sm.nbase[1];
+    issue_next<kEmit>(nx, in, in_bias, in_off, out_off, cur + m, L1, i_nxt, i_end, tid);
+    if (kEmit && pending) store_out(pd_o, (const uint8_t *)sm.out_w, pd_lo, pd_hi, tid, kT);
+    pending = false;
+    if (oversized) {
+      if (tid == 0) encode_literal_global<kEmit>(ia, i_nxt - i_cur, oa, sm.code, enc_len + cur);
+    } else {
+      const uint32_t out_bytes = kEmit ? sm.rec[m] >> 16 : 0u;
+      if (kEmit) {
+        __syncthreads();  // out_w has been read by the flush
         for (uint32_t c = tid; c < (out_bytes + 15u) >> 4; c += kT) *(u32x4 *)(sm.out_w + 4u * c) = u32x4{0u, 0u, 0u, 0u};
+      }
       // counting sort by plaintext length
       uint32_t bk = 0, rk = 0;
       if (tid < m) {
-        const uint32_t bytes = sm.rec[tid + 1].x - sm.rec[tid].x;
+        const uint32_t bytes = (sm.rec[tid + 1] & 0xffffu) - (sm.rec[tid] & 0xffffu);
         bk = bytes < 32u ? bytes : min(32u + ((bytes - 32u) >> 4), (uint32_t)kBuckets - 1u);
         rk = atomicAdd(&sm.hist[bk], 1u);
       }
@@ -323,19 +285,21 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu((kT / 64 * M
       __syncthreads();
       if (tid < m) {
         const uint32_t lit = sm.order[tid];
-        const uint2 r0 = sm.rec[lit], r1 = sm.rec[lit + 1];
-        const uint32_t bits = encode_one<kEmit>(sm, r0.x, r1.x, r0.y);
-        if (!kEmit) enc_len[s + cur + lit] = (bits + 7u) >> 3;
+        const uint32_t r0 = sm.rec[lit], r1 = sm.rec[lit + 1];
+        const uint32_t bits = encode_one<kEmit>(sm, r0 & 0xffffu, r1 & 0xffffu, r0 >> 16);
+        if (!kEmit) enc_len[cur + lit] = (bits + 7u) >> 3;
       }
+      __syncthreads();  // in_w free, out_w complete
       if (kEmit) {
-        __syncthreads();
         pd_o = oa - odelta;
         pd_lo = odelta;
         pd_hi = out_bytes;
         pending = true;
       }
-      cur = end;
     }
+    cur += m;
+    i_cur = i_nxt;
+    o_cur = o_nxt;
   }
   if (kEmit && pending) store_out(pd_o, (const uint8_t *)sm.out_w, pd_lo, pd_hi, tid, kT);
 }
@@ -345,18 +309,18 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu((kT / 64 * M
 hipError_t launch_encode_len(const DevTables &t, const uint8_t *in, const uint64_t *in_off, uint64_t in_bias,
                              uint64_t n, uint32_t *enc_len, hipStream_t s) {
   if (n == 0) return hipSuccess;
-  const uint64_t ntiles = (n + kT - 1) / kT;
-  encode_kernel<false><<<dim3(dev::tile_grid(ntiles, 1, MHQ_ENC_BLOCKS * MHQ_PER_CU)), dim3(kT), 0, s>>>(
-      in, in_off, in_bias, n, nullptr, nullptr, 0, enc_len, t.code, t.len, ntiles);
+  const unsigned grid = dev::tile_grid((n + kT - 1) / kT, 1, MHQ_ENC_BLOCKS * MHQ_PER_CU);
+  encode_kernel<false><<<dim3(grid), dim3(kT), 0, s>>>(in, in_off, in_bias, n, nullptr, nullptr, 0, enc_len, t.code,
+                                                        t.len, (n + grid - 1) / grid);
   return hipGetLastError();
 }
 
 hipError_t launch_encode(const DevTables &t, const uint8_t *in, const uint64_t *in_off, uint64_t in_bias,
                          uint64_t n, uint8_t *out, const uint64_t *out_off, uint64_t out_bias, hipStream_t s) {
   if (n == 0) return hipSuccess;
-  const uint64_t ntiles = (n + kT - 1) / kT;
-  encode_kernel<true><<<dim3(dev::tile_grid(ntiles, 1, MHQ_ENC_BLOCKS * MHQ_PER_CU)), dim3(kT), 0, s>>>(
-      in, in_off, in_bias, n, out, out_off, out_bias, nullptr, t.code, t.len, ntiles);
+  const unsigned grid = dev::tile_grid((n + kT - 1) / kT, 1, MHQ_ENC_BLOCKS * MHQ_PER_CU);
+  encode_kernel<true><<<dim3(grid), dim3(kT), 0, s>>>(in, in_off, in_bias, n, out, out_off, out_bias, nullptr, t.code,
+                                                       t.len, (n + grid - 1) / grid);
   return hipGetLastError();
 }
 
