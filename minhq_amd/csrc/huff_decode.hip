@@ -159,8 +159,10 @@ __device__ __forceinline__ uint32_t decode_one(Smem &sm, uint32_t p, uint32_t en
   const uint32_t ostart = optr;
   uint32_t acc = 0;  // this literal's bytes of word optr>>2 below optr
   uint32_t bad = 0;
-  const bool roomy = oend - optr >= (endbit - p) / 5u;
-  while (roomy && endbit - p >= 62u) {
+  // The fast loop stops (without consuming) at an EOS prefix; the checked
+  // loop below then reports it.
+  bool go = oend - optr >= (endbit - p) / 5u;
+  while (go && endbit - p >= 62u) {
     const uint32_t w0 = optr >> 2;
     uint64_t o64 = acc;
 #pragma unroll
@@ -170,21 +172,19 @@ __device__ __forceinline__ uint32_t decode_one(Smem &sm, uint32_t p, uint32_t en
       uint32_t ns = e >> 26, tot = (e >> 21) & 31u, syms = e & 0xffffu;
       if (ns == 0) {
         tot = long_code(sm, win, syms);
-        ns = 1;
-        bad |= tot == 0;
+        ns = tot ? 1u : 0u;
+        syms = tot ? syms : 0u;
+        go = go && tot != 0;
       }
-      if (!bad) {
-        o64 |= (uint64_t)syms << ((optr - 4u * w0) * 8u);
-        optr += ns;
-        p += tot;
-      }
+      o64 |= (uint64_t)syms << ((optr - 4u * w0) * 8u);
+      optr += ns;
+      p += tot;
     }
     if (o64) {
       atomicOr(&sm.out_w[w0], (uint32_t)o64);
       atomicOr(&sm.out_w[w0 + 1], (uint32_t)(o64 >> 32));
     }
     acc = (optr >> 2) != w0 ? (uint32_t)(o64 >> 32) : (uint32_t)o64;
-    if (bad) return (optr - ostart) | (1u << 31);
   }
   bool fin = false;
   while (!fin) {
@@ -405,7 +405,7 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu((kT / 64 * M
       uint32_t bk = 0, rk = 0;
       if (tid < m) {
         const uint32_t bytes = (sm.rec[tid + 1] & 0xffffu) - (sm.rec[tid] & 0xffffu);
-        bk = bytes < 32u ? bytes : min(32u + ((bytes - 32u) >> 4), (uint32_t)kBuckets - 1u);
+        bk = bytes < 48u ? bytes : min(48u + ((bytes - 48u) >> 3), (uint32_t)kBuckets - 1u);
         rk = atomicAdd(&sm.hist[bk], 1u);
       }
       __syncthreads();

@@ -266,7 +266,7 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu((kT / 64 * M
       uint32_t bk = 0, rk = 0;
       if (tid < m) {
         const uint32_t bytes = (sm.rec[tid + 1] & 0xffffu) - (sm.rec[tid] & 0xffffu);
-        bk = bytes < 32u ? bytes : min(32u + ((bytes - 32u) >> 4), (uint32_t)kBuckets - 1u);
+        bk = bytes < 48u ? bytes : min(48u + ((bytes - 48u) >> 3), (uint32_t)kBuckets - 1u);
         rk = atomicAdd(&sm.hist[bk], 1u);
       }
       __syncthreads();

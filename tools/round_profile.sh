@@ -11,7 +11,7 @@ mkdir -p "$OUT"
 BENCH="bench.py --steps 20 --warmup 5"
 timeout -k 10 600 python3 $BENCH --cpu-seconds 15 > "$OUT/bench.json" 2> "$OUT/bench.err" || { echo "bench failed"; tail "$OUT/bench.err"; exit 1; }
 cat "$OUT/bench.json"
-timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/stats" -o run -- python3 $BENCH --no-cpu \
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/stats" -o run -- python3 $BENCH --no-cpu --no-extras \
   > "$OUT/stats.log" 2>&1 || { echo "stats pass failed"; tail "$OUT/stats.log"; exit 1; }
 echo "stats ok"
 timeout -k 10 600 rocprofv3 --kernel-trace --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o run -- python3 $BENCH --no-cpu --no-extras \
