@@ -146,14 +146,14 @@ __device__ __forceinline__ uint32_t long_code(const Smem &sm, uint32_t win, uint
 // Decodes staged literal bits [p, endbit) into staging bytes [optr, oend).
 // Returns out_len | status << 31.
 //
-// Fast loop: while at least 62 bits remain, two probes (each <= 30 bits) read
-// windows that lie wholly inside the literal, and when the output region can
-// hold floor(bits/5) bytes (the most any input can produce) no probe needs a
-// room or end check: every probe emits its one or two symbols (LUT1 keeps the
-// second symbol 0 for one-symbol entries, so OR-ing 16 bits is exact).  The
-// last bits, and literals with a truncating output region, take the checked
-// loop.  A probe that meets 30 ones before the end here is always INVALID:
-// more than 30 bits remain and the output is not full.
+// Fast loop: a probe made with at least 32 bits left sees only this literal's
+// bits, and when the output region can hold floor(bits/5) bytes (the most any
+// input can produce) it needs no room or end check: it emits its one or two
+// symbols (LUT1 keeps the second symbol 0 for one-symbol entries, so OR-ing 16
+// bits is exact).  Two probes per iteration, the second one masked off when
+// fewer than 32 bits are left.  An EOS prefix stops the fast loop without
+// consuming it.  The last (< 32) bits, EOS prefixes and literals with a
+// truncating output region take the checked loop.
 __device__ __forceinline__ uint32_t decode_one(Smem &sm, uint32_t p, uint32_t endbit, uint32_t optr,
                                                uint32_t oend) {
   const uint32_t ostart = optr;
@@ -162,15 +162,17 @@ __device__ __forceinline__ uint32_t decode_one(Smem &sm, uint32_t p, uint32_t en
   // The fast loop stops (without consuming) at an EOS prefix; the checked
   // loop below then reports it.
   bool go = oend - optr >= (endbit - p) / 5u;
-  while (go && endbit - p >= 62u) {
+  while (go && endbit - p >= 32u) {
     const uint32_t w0 = optr >> 2;
     uint64_t o64 = acc;
 #pragma unroll
     for (int u = 0; u < 2; u++) {
+      // a probe with >= 32 bits left sees only this literal's bits
+      const bool ok = u == 0 || endbit - p >= 32u;
       const uint32_t win = window_at(sm.in_w, p);
-      const uint32_t e = sm.lut1[win >> (32 - kLut1Bits)];
+      const uint32_t e = ok ? sm.lut1[win >> (32 - kLut1Bits)] : 0u;
       uint32_t ns = e >> 26, tot = (e >> 21) & 31u, syms = e & 0xffffu;
-      if (ns == 0) {
+      if (ns == 0 && ok) {
         tot = long_code(sm, win, syms);
         ns = tot ? 1u : 0u;
         syms = tot ? syms : 0u;
