@@ -9,42 +9,49 @@
 //     (hc/huffman.go:63-76): one more bit of input is "invalid Huffman coding";
 //   * Read stops as soon as its buffer is full (hc/huffman.go:104).
 //
-// Structure: one workgroup of kT threads owns a block tile of kT consecutive
-// literals and decodes it with one thread per literal.
-//   * staging: the tile's offsets (one coalesced u64 per thread), its input
-//     bytes (aligned 16-B loads, byte-swapped, reverse word order so that the
-//     logical word pair {k+1, k} is one little-endian u64) and its output
-//     region (zero-filled, global layout) live in LDS; the output leaves as
-//     aligned 16-B stores, out_len/status as coalesced stores;
-//   * balance: a counting sort by encoded length gives thread t the literal
-//     of rank t, so the 64 literals of a wave have similar lengths and the
-//     wave's loop runs about as long as its average literal;
-//   * occupancy: two workgroups per CU (2 x kT/64 waves) hide the LDS round
-//     trips of the per-literal decode chains;
-//   * a probe reads LUT1 with the next 12 bits (one or two codes of <= 12
-//     bits) or, for longer codes, LUT2 by count of leading ones; output bytes
-//     are packed into registers on the LDS word grid and OR-ed into the zeroed
-//     staging words, so literals that share a word need no ordering.
-//   * a tile whose bytes exceed the staging slices is processed as several
-//     sub-tiles; a single literal larger than a slice is decoded by one
-//     thread straight from global memory.
+// Structure: one workgroup per CU; its waves work independently (no
+// workgroup barrier after the table load).  A wave takes a tile of up to 128
+// consecutive literals at a time (tiles handed out by an LDS counter) and
+// decodes it with two literals per lane:
+//   * staging: the tile's offsets and input bytes are loaded into registers
+//     one tile ahead (offsets two tiles ahead), so HBM latency hides behind
+//     the decode of the current tile.  Input lands in the wave's LDS slice as
+//     byte-swapped words (word k = stream bits 32k..32k+31, MSB first); the
+//     output is assembled in a zeroed LDS copy of the tile's output region
+//     (global layout) and leaves as aligned 16-B stores, with out_len/status
+//     as coalesced stores, when the next tile starts;
+//   * balance: a counting sort by encoded length (descending) inside the
+//     wave; lane t decodes rank t, then rank 127-t, so every lane's two
+//     literals add up to about the same length and the 64 lanes of a wave
+//     run loops of about the same length;
+//   * a literal's bits stream through a 64-bit register buffer refilled one
+//     staged word at a time; a probe reads LUT1 with the next 12 bits (one or
+//     two codes of <= 12 bits) or, for longer codes, LUT2 by count of leading
+//     ones; output bytes gather in a 64-bit register and are OR-ed into the
+//     staging one word per step, so literals that share a word need no
+//     ordering;
+//   * a tile too large for the slices is decoded in pieces that fit; a single
+//     literal larger than a slice is decoded by one lane straight from global
+//     memory.
 #include <hip/hip_runtime.h>
+
+#include <algorithm>
 
 #include "huff_common.h"
 #include "huff_kernels.h"
 #include "huff_table.h"
 
-#ifndef MHQ_DEC_T  // threads per block
-#define MHQ_DEC_T 768
+#ifndef MHQ_DEC_WAVES  // waves per workgroup (one workgroup per CU)
+#define MHQ_DEC_WAVES 12
 #endif
-#ifndef MHQ_DEC_INCAP  // staging slices (bytes)
-#define MHQ_DEC_INCAP 22528
+#ifndef MHQ_DEC_TILE  // most literals per wave tile (64 < tile <= 128)
+#define MHQ_DEC_TILE 128
 #endif
-#ifndef MHQ_DEC_OUTCAP
-#define MHQ_DEC_OUTCAP 34816
+#ifndef MHQ_DEC_PF  // 16-B input chunks per lane staged from registers: a wave's input slice is 1 KiB * PF
+#define MHQ_DEC_PF 4
 #endif
-#ifndef MHQ_DEC_BLOCKS  // resident workgroups per CU
-#define MHQ_DEC_BLOCKS 2
+#ifndef MHQ_DEC_WOUT  // a wave's output slice (bytes, multiple of 16)
+#define MHQ_DEC_WOUT 6448
 #endif
 
 namespace mhq {
@@ -52,34 +59,48 @@ namespace {
 
 using namespace dev;
 
-constexpr int kT = MHQ_DEC_T;
-constexpr int kInCap = MHQ_DEC_INCAP;    // staged input bytes (incl. 16-B alignment slack)
-constexpr int kOutCap = MHQ_DEC_OUTCAP;  // staged output bytes
-constexpr uint32_t kInWords = kInCap / 4 + 4;
-constexpr int kPF = (kInCap / 16 + kT - 1) / kT;  // prefetched input chunks per thread
-#ifdef MHQ_DEC_NOPF  // prefetch only the next tile's offsets, stage its input on arrival
-constexpr bool kPrefetchInput = false;
-#else
-constexpr bool kPrefetchInput = true;
-#endif
+constexpr int kWaves = MHQ_DEC_WAVES;
+constexpr int kT = kWaves * kWave;
+constexpr int kTile = MHQ_DEC_TILE;  // most literals per wave tile
+static_assert(kTile > kWave && kTile <= 2 * kWave, "a lane decodes one or two literals of a tile");
+constexpr int kPF = MHQ_DEC_PF;
+constexpr int kWIn = kPF * kWave * 16;  // input slice bytes (from the tile's 16-B aligned start)
+constexpr int kWOut = MHQ_DEC_WOUT;     // output slice bytes (from the tile's 16-B aligned start)
 constexpr int kBuckets = 64;
+static_assert(kWOut % 16 == 0, "output slice must be whole 16-B chunks");
+
+struct WaveSmem {
+  uint32_t in_w[kWIn / 4 + 4];    // stream words, byte-swapped; +4 words of look-ahead slack
+  uint32_t out_w[kWOut / 4 + 4];  // output staging (global layout, zero-filled); +4 words slack
+  uint32_t rec[kTile + 1];        // per boundary: input byte index | output byte index << 16
+  uint32_t len[kTile];            // out_len | status << 31, by literal
+  uint32_t hist[kBuckets];
+  uint8_t order[kTile];  // literals by descending encoded length
+};
 
 struct Smem {
   uint32_t lut1[kLut1Size];
   uint16_t lut2[kLut2Size];
-  uint32_t in_w[kInWords];          // stream words, byte-swapped, reverse word order
-  uint32_t out_w[kOutCap / 4 + 4];  // output staging (global layout, zero-filled)
-  uint32_t rec[kT + 1];             // per boundary: input byte index | output byte index << 16
-  uint16_t order[kT];               // literals by ascending encoded length
-  uint32_t hist[kBuckets];
-  uint64_t nbase[2];                // in_off / out_off at the next sub-tile's first literal
+  uint8_t clen[256];  // code length per symbol (len0 of a LUT1 entry, for the checked loop)
+  uint32_t next_tile;
+  WaveSmem w[kWaves];
 };
 
-// One literal, one thread, straight from global memory: literals too large for
+// A code of 13..30 bits, or the all-ones EOS prefix (c >= 30), at the top of
+// the 32 stream bits `win`: its symbol and length, length 0 for the EOS prefix.
+__device__ __forceinline__ uint32_t long_code(const uint16_t *lut2, uint32_t win, uint32_t &sym) {
+  const uint32_t nw = ~win;
+  const uint32_t c = nw ? (uint32_t)__builtin_clz(nw) : 32u;
+  if (c >= (uint32_t)kEosOnes) return 0;
+  const uint32_t e2 = lut2[(c << kLut2SubBits) | ((win << (c + 1)) >> (32 - kLut2SubBits))];
+  sym = e2 & 0xffu;
+  return e2 >> 8;
+}
+
+// One literal, one lane, straight from global memory: literals too large for
 // the staging slices.  Same decision rules as the staged loop.
 __device__ void decode_literal_global(const uint8_t *src, uint64_t nbytes, uint8_t *dst, uint64_t cap,
-                                      const uint32_t *lut1, const uint16_t *lut2, uint32_t *out_len,
-                                      uint8_t *status) {
+                                      const Smem &sm, uint32_t *out_len, uint8_t *status) {
   const uintptr_t a0 = (uintptr_t)src & ~(uintptr_t)3;
   const uint32_t *wb = (const uint32_t *)a0;
   const uint64_t bit0 = ((uintptr_t)src & 3u) * 8u;
@@ -94,27 +115,26 @@ __device__ void decode_literal_global(const uint8_t *src, uint64_t nbytes, uint8
     const uint32_t w0 = __builtin_bswap32(wb[k < lastw ? k : lastw]);
     const uint32_t w1 = __builtin_bswap32(wb[k + 1 < lastw ? k + 1 : lastw]);
     const uint32_t win = s ? (w0 << s) | (w1 >> (32u - s)) : w0;
-    const uint32_t e = lut1[win >> (32 - kLut1Bits)];
-    const uint32_t nsym = e >> 26;
-    if (nsym == 0) {
+    const uint32_t e = sm.lut1[win >> (32 - kLut1Bits)];
+    if (e == 0) {  // a long code or the EOS prefix
       const uint32_t nw = ~win;
       const uint32_t c = nw ? (uint32_t)__builtin_clz(nw) : 32u;
       if (c >= (uint32_t)kEosOnes) {
         st = rem > (uint64_t)kEosOnes;
         break;
       }
-      const uint32_t e2 = lut2[(c << kLut2SubBits) | ((win << (c + 1)) >> (32 - kLut2SubBits))];
-      const uint32_t L = e2 >> 8;
+      uint32_t sym = 0;
+      const uint32_t L = long_code(sm.lut2, win, sym);
       if (L == 0 || L > rem) break;
-      dst[n++] = (uint8_t)e2;
+      dst[n++] = (uint8_t)sym;
       p += L;
       continue;
     }
-    const uint32_t len0 = (e >> 16) & 31u, tot = (e >> 21) & 31u;
+    const uint32_t tot = e & 0xffu, s0 = (e >> 16) & 0xffu, len0 = sm.clen[s0];
     if (len0 > rem) break;
-    dst[n++] = (uint8_t)e;
-    if (nsym == 2 && tot <= rem && n < cap) {
-      dst[n++] = (uint8_t)(e >> 8);
+    dst[n++] = (uint8_t)s0;
+    if (((e >> 8) & 0xffu) == 16u && tot <= rem && n < cap) {
+      dst[n++] = (uint8_t)(e >> 24);
       p += tot;
     } else {
       p += len0;
@@ -124,141 +144,230 @@ __device__ void decode_literal_global(const uint8_t *src, uint64_t nbytes, uint8
   *status = st;
 }
 
-// The 32 stream bits at bit position p (one ds_read2_b32 of logical words k, k+1).
-__device__ __forceinline__ uint32_t window_at(const uint32_t *in_w, uint32_t p) {
-  const uint32_t k = p >> 5, sh = p & 31u;
-  const uint32_t *wp = in_w + (kInWords - 2u - k);
-  const uint64_t ww = (uint64_t)wp[0] | ((uint64_t)wp[1] << 32);  // {word k+1, word k}
-  return (uint32_t)((ww << sh) >> 32);
-}
-
-// A code of 13..30 bits, or the all-ones EOS prefix (c >= 30): its symbol and
-// length, length 0 for the EOS prefix.
-__device__ __forceinline__ uint32_t long_code(const Smem &sm, uint32_t win, uint32_t &sym) {
-  const uint32_t nw = ~win;
-  const uint32_t c = nw ? (uint32_t)__builtin_clz(nw) : 32u;
-  if (c >= (uint32_t)kEosOnes) return 0;
-  const uint32_t e2 = sm.lut2[(c << kLut2SubBits) | ((win << (c + 1)) >> (32 - kLut2SubBits))];
-  sym = e2 & 0xffu;
-  return e2 >> 8;
-}
-
-// Decodes staged literal bits [p, endbit) into staging bytes [optr, oend).
-// Returns out_len | status << 31.
-//
-// Fast loop: a probe made with at least 32 bits left sees only this literal's
-// bits, and when the output region can hold floor(bits/5) bytes (the most any
-// input can produce) it needs no room or end check: it emits its one or two
-// symbols (LUT1 keeps the second symbol 0 for one-symbol entries, so OR-ing 16
-// bits is exact).  Two probes per iteration, the second one masked off when
-// fewer than 32 bits are left.  An EOS prefix stops the fast loop without
-// consuming it.  The last (< 32) bits, EOS prefixes and literals with a
-// truncating output region take the checked loop.
-__device__ __forceinline__ uint32_t decode_one(Smem &sm, uint32_t p, uint32_t endbit, uint32_t optr,
-                                               uint32_t oend) {
-  const uint32_t ostart = optr;
-  uint32_t acc = 0;  // this literal's bytes of word optr>>2 below optr
-  uint32_t bad = 0;
-  // The fast loop stops (without consuming) at an EOS prefix; the checked
-  // loop below then reports it.
-  bool go = oend - optr >= (endbit - p) / 5u;
-  while (go && endbit - p >= 32u) {
-    const uint32_t w0 = optr >> 2;
-    uint64_t o64 = acc;
-#pragma unroll
-    for (int u = 0; u < 2; u++) {
-      // a probe with >= 32 bits left sees only this literal's bits
-      const bool ok = u == 0 || endbit - p >= 32u;
-      const uint32_t win = window_at(sm.in_w, p);
-      const uint32_t e = ok ? sm.lut1[win >> (32 - kLut1Bits)] : 0u;
-      uint32_t ns = e >> 26, tot = (e >> 21) & 31u, syms = e & 0xffffu;
-      if (ns == 0 && ok) {
-        tot = long_code(sm, win, syms);
-        ns = tot ? 1u : 0u;
-        syms = tot ? syms : 0u;
-        go = go && tot != 0;
-      }
-      o64 |= (uint64_t)syms << ((optr - 4u * w0) * 8u);
-      optr += ns;
-      p += tot;
-    }
-    if (o64) {
-      atomicOr(&sm.out_w[w0], (uint32_t)o64);
-      atomicOr(&sm.out_w[w0 + 1], (uint32_t)(o64 >> 32));
-    }
-    acc = (optr >> 2) != w0 ? (uint32_t)(o64 >> 32) : (uint32_t)o64;
+// Output bytes in registers: `acc` holds the bytes from 4*ow up, `ab` bits of
+// it are decided.  The low word is OR-ed into the zeroed staging every step
+// (idempotent), so words shared with a neighbouring literal need no ordering.
+struct OutAcc {
+  uint64_t acc;
+  uint32_t ow, ab;
+  __device__ __forceinline__ void init(uint32_t optr) {
+    acc = 0;
+    ow = optr >> 2;
+    ab = (optr & 3u) * 8u;
   }
+  __device__ __forceinline__ void put(uint32_t syms, uint32_t nbits) {
+    acc |= (uint64_t)syms << ab;
+    ab += nbits;
+  }
+  __device__ __forceinline__ void flush(uint32_t *out_w) {
+#if defined(MHQ_X_PLAINW)  // timing experiment only (wrong output)
+    out_w[ow] = (uint32_t)acc;
+#elif !defined(MHQ_X_NOOR)
+    atomicOr(&out_w[ow], (uint32_t)acc);
+#endif
+    acc >>= ab & 32u;  // a completed word leaves
+    ow += ab >> 5;
+    ab &= 31u;
+  }
+  __device__ __forceinline__ uint32_t optr() const { return ow * 4u + (ab >> 3); }
+};
+
+// A literal's stream bits in registers: `bb` holds bits [p, kb) MSB-aligned
+// (zeros below); `w` is staged word kb/32, read ahead.
+struct BitBuf {
+  uint64_t bb;
+  uint32_t p, kb, w;
+  const uint32_t *in_w;
+
+  __device__ __forceinline__ void init(const uint32_t *words, uint32_t p0) {
+    in_w = words;
+    p = p0;
+    const uint32_t k = p0 >> 5;
+    bb = (((uint64_t)in_w[k] << 32) | in_w[k + 1]) << (p0 & 31u);
+    kb = (k + 2u) * 32u;
+    w = in_w[k + 2u];
+  }
+  // Tops the buffer up to >= 33 valid bits when it holds <= 32 (branch free;
+  // the look-ahead word is re-read either way).
+  __device__ __forceinline__ void refill() {
+    const uint32_t nb = kb - p;
+    const bool need = nb <= 32u;
+    bb |= (uint64_t)(need ? w : 0u) << ((32u - nb) & 63u);
+    kb += need ? 32u : 0u;
+    w = in_w[kb >> 5];
+  }
+  __device__ __forceinline__ uint32_t top32() const { return (uint32_t)(bb >> 32); }
+  // Takes the bit count from an entry's low byte (the shift uses bits [5:0]).
+  __device__ __forceinline__ void consume(uint32_t e) {
+    bb <<= (e & 63u);
+    p += e & 0xffu;
+  }
+};
+
+// One fast step at bit p of a literal ending at endbit (p + 24 <= endbit):
+// two LUT1 probes (<= 12 bits each) with no end or room check.  A long code
+// or the EOS prefix has entry 0, which consumes and emits nothing, so the
+// second probe meets it again: one check per step resolves it through LUT2.
+// The EOS prefix (INVALID when a 31st bit follows) and a long code running
+// past the end both finish the literal: `lim` = -1 ends the fast loop and
+// `bad` carries the status.
+__device__ __forceinline__ void fast_step(const Smem &sm, WaveSmem &ws, BitBuf &in, OutAcc &out, uint32_t endbit,
+                                          int &lim, uint32_t &bad) {
+#ifdef MHQ_X_NOLUT  // timing experiment only (wrong output): every probe is a 2-symbol 10-bit entry
+  uint32_t e = lut1_entry(97, 97, 10, 2) ^ (in.top32() & 0x07070000u);
+#else
+  uint32_t e = sm.lut1[in.top32() >> (32 - kLut1Bits)];
+#endif
+  out.put(e >> 16, (e >> 8) & 0xffu);
+  in.consume(e);
+#ifdef MHQ_X_NOLUT
+  e = lut1_entry(97, 97, 10, 2) ^ (in.top32() & 0x07070000u);
+#else
+  e = sm.lut1[in.top32() >> (32 - kLut1Bits)];
+#endif
+  if (e == 0) {  // a long code or the EOS prefix (the first probe, if it met one, took nothing)
+    in.refill();
+    uint32_t sym = 0;
+    const uint32_t L = long_code(sm.lut2, in.top32(), sym);
+    const uint32_t left = endbit - in.p;
+    if (L == 0 || L > left) {
+      bad = L == 0 && left > (uint32_t)kEosOnes;  // a 31st bit exists: nil child (hc/huffman.go:111-113)
+      lim = -1;
+    } else {
+      e = L | (8u << 8) | (sym << 16);
+    }
+  }
+  out.put(e >> 16, (e >> 8) & 0xffu);
+  in.consume(e);
+  in.refill();
+  out.flush(ws.out_w);
+}
+
+// The last (< 24) bits of a literal whose output region is not truncating:
+// single probes while >= 12 bits are left, then one checked probe, which
+// decodes every code that still fits (three codes need >= 15 bits; a long
+// code cannot fit).  No EOS prefix can be INVALID here (that needs > 30 bits).
+// Returns out_len.
+__device__ __forceinline__ uint32_t decode_end(const Smem &sm, WaveSmem &ws, uint32_t p, uint32_t endbit,
+                                               uint32_t optr, uint32_t ostart) {
+  BitBuf in;
+  in.init(ws.in_w, p);
+  OutAcc out;
+  out.init(optr);
+  bool more = true;
+  while (more && in.p + 12u <= endbit) {
+    uint32_t e = sm.lut1[in.top32() >> (32 - kLut1Bits)];
+    if (e == 0) {
+      uint32_t sym = 0;
+      const uint32_t L = long_code(sm.lut2, in.top32(), sym);
+      more = L != 0 && L <= endbit - in.p;
+      e = more ? (L | (8u << 8) | (sym << 16)) : 0u;
+    }
+    out.put(e >> 16, (e >> 8) & 0xffu);
+    in.consume(e);
+    in.refill();
+    out.flush(ws.out_w);
+  }
+  if (more) {
+    const uint32_t e = sm.lut1[in.top32() >> (32 - kLut1Bits)];
+    const uint32_t left = endbit - in.p;
+    const uint32_t len0 = sm.clen[(e >> 16) & 0xffu];
+    const uint32_t c8 = e == 0 ? 0u : ((e & 0xffu) <= left ? (e >> 8) & 0xffu : (len0 <= left ? 8u : 0u));
+    out.put(__builtin_amdgcn_ubfe(e >> 16, 0, c8), c8);
+  }
+  atomicOr(&ws.out_w[out.ow], (uint32_t)out.acc);
+  if (out.ab > 32u) atomicOr(&ws.out_w[out.ow + 1], (uint32_t)(out.acc >> 32));
+  return out.optr() - ostart;
+}
+
+// The general checked loop (literals with a truncating output region):
+// decodes literal bits [p, endbit) into staging bytes [optr, oend) one probe
+// at a time, with the reference's end-of-literal and buffer-full rules
+// (hc/huffman.go:102-121).  Returns out_len | status << 31.
+__device__ __noinline__ uint32_t decode_checked(const Smem &sm, WaveSmem &ws, uint32_t p, uint32_t endbit,
+                                                uint32_t optr, uint32_t oend) {
+  BitBuf in;
+  in.init(ws.in_w, p);
+  OutAcc out;
+  out.init(optr);
+  const uint32_t ostart = optr;
+  uint32_t bad = 0;
   bool fin = false;
   while (!fin) {
-    const uint32_t w0 = optr >> 2;
-    uint64_t o64 = acc;
-#pragma unroll
-    for (int u = 0; u < 2; u++) {  // two probes per output flush
-      const uint32_t win = window_at(sm.in_w, p);
-      const uint32_t rem = endbit - p;
-      const uint32_t e = sm.lut1[win >> (32 - kLut1Bits)];
-      uint32_t len0 = (e >> 16) & 31u, tot = (e >> 21) & 31u, ns = e >> 26, syms = e & 0xffffu;
-      if (ns == 0) {
-        const uint32_t L = long_code(sm, win, syms);
-        len0 = tot = L ? L : 0xffffffffu;  // the EOS prefix never fits: the literal ends here
-        ns = 1;
-        bad |= L == 0 && rem > (uint32_t)kEosOnes;  // a 31st bit exists: nil child
-      }
-      const bool ct = tot <= rem;
-      uint32_t cnt = ct ? ns : (len0 <= rem ? 1u : 0u);
-      const uint32_t room = oend - optr;  // Read() stops once p is full (hc/huffman.go:104)
-      cnt = cnt < room ? cnt : room;
-      cnt = fin ? 0u : cnt;
-      o64 |= (uint64_t)__builtin_amdgcn_ubfe(syms, 0, cnt * 8u) << ((optr - 4u * w0) * 8u);
-      optr += cnt;
-      p += cnt ? (ct ? tot : len0) : 0u;
-      fin |= cnt == 0;
+    in.refill();
+    const uint32_t win = in.top32();
+    const uint32_t left = endbit - in.p;
+    const uint32_t e = sm.lut1[win >> (32 - kLut1Bits)];
+    uint32_t tot = e & 0xffu, ns8 = (e >> 8) & 0xffu, syms = e >> 16, len0 = sm.clen[(e >> 16) & 0xffu];
+    if (e == 0) {
+      const uint32_t L = long_code(sm.lut2, win, syms);
+      len0 = tot = L ? L : 0xffffffffu;  // the EOS prefix never fits: the literal ends here
+      ns8 = 8u;
+      bad |= L == 0 && left > (uint32_t)kEosOnes;  // a 31st bit exists: nil child
     }
-    if (o64) {
-      atomicOr(&sm.out_w[w0], (uint32_t)o64);
-      atomicOr(&sm.out_w[w0 + 1], (uint32_t)(o64 >> 32));
-    }
-    acc = (optr >> 2) != w0 ? (uint32_t)(o64 >> 32) : (uint32_t)o64;
+    uint32_t c8 = tot <= left ? ns8 : (len0 <= left ? 8u : 0u);
+    const uint32_t room = oend - out.optr();  // Read() stops once p is full (hc/huffman.go:104)
+    c8 = room >= 2u ? c8 : min(c8, room * 8u);
+    const uint32_t cons = c8 == 16u ? tot : (c8 ? len0 : 0u);
+    out.put(__builtin_amdgcn_ubfe(syms, 0, c8), c8);
+    in.bb <<= cons & 63u;
+    in.p += cons;
+    fin = c8 == 0;
+    out.flush(ws.out_w);
   }
-  bad = optr != oend ? bad : 0u;
-  return (optr - ostart) | (bad << 31);
+  const uint32_t oend_got = out.optr();
+  bad = oend_got != oend ? bad : 0u;
+  return (oend_got - ostart) | (bad << 31);
 }
 
-#ifdef MHQ_DIAG_STAMPS  // diagnostic build: shader cycles per phase, summed over waves
-__device__ unsigned long long g_diag[8];
-__device__ __forceinline__ unsigned long long stamp_now() {
-  unsigned long long t;
-  __builtin_amdgcn_sched_barrier(0);
-  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
-  __builtin_amdgcn_sched_barrier(0);
-  return t;
-}
-#define STAMP(i)                                    \
-  do {                                              \
-    const unsigned long long _t = stamp_now();      \
-    ph[i] += _t - t_last;                           \
-    t_last = _t;                                    \
+// A literal's place in the staged tile.
+struct LitRef {
+  uint32_t lit, p, endbit, optr, oend;
+  __device__ __forceinline__ void load(const WaveSmem &ws, uint32_t l) {
+    lit = l;
+    const uint32_t r0 = ws.rec[l], r1 = ws.rec[l + 1];
+    p = (r0 & 0xffffu) * 8u;
+    endbit = (r1 & 0xffffu) * 8u;
+    optr = r0 >> 16;
+    oend = r1 >> 16;
+  }
+  // The output region holds floor(bits/5) bytes, the most any input can
+  // produce: no room check is needed.
+  __device__ __forceinline__ bool roomy() const { return oend - optr >= (endbit - p) / 5u; }
+};
+
+#ifdef MHQ_DIAG_COUNT
+__device__ unsigned long long g_cnt[8];
+#endif
+#ifdef MHQ_DIAG_TIMELINE  // diagnostic build: per-wave timeline (s_memrealtime, 100 MHz)
+constexpr int kTlSlots = 64;  // per wave: [0] start, [63] end, tile j < 20: 1 + 3j + {0 staged, 1 flushed, 2 decoded}
+__device__ unsigned long long g_tl[1024 * 16 * kTlSlots];
+#define TL(slot)                                                                                          \
+  do {                                                                                                    \
+    const int _s = (slot);                                                                                \
+    if (lane == 0 && _s < kTlSlots) g_tl[(blockIdx.x * 16 + wave) * kTlSlots + _s] = wall_clock64();     \
   } while (0)
 #else
-#define STAMP(i) \
+#define TL(slot) \
   do {           \
   } while (0)
 #endif
 
-// ---- a block's literals: one contiguous range, greedy sub-tiles ----------
-// Block b owns literals [b*R, (b+1)*R) (R = ceil(n / grid)).  A sub-tile is
-// the longest run of at most kT literals from `cur` whose input and output
-// fit the staging slices, so tiles stay full whatever the length mix.
+// ---- per-wave tiles ------------------------------------------------------
+// Workgroup b owns literals [L0, L1) = [b*R, (b+1)*R); tile t of it is
+// literals L0 + 128t + [0, 128).  Wave w starts with tiles w and w + kWaves,
+// then takes tiles from the LDS counter.
 //
-// Software pipeline: as soon as a sub-tile's extent is known, the offsets and
-// the first kInCap input bytes of the next one are issued into registers, so
-// they load while this one decodes.  Rules that keep the loads asynchronous:
-//   * only raw loaded values are kept; no arithmetic, select or copy touches
-//     them before they are consumed at the top of the next sub-tile;
-//   * loads are unconditional (clamped addresses);
-//   * gfx9 counts stores in vmcnt too, so waiting for a load also waits for
-//     every store issued before it.  A sub-tile's output is therefore stored
-//     only after the next sub-tile's loads have been issued.
+// Pipeline, per wave: while tile k decodes, tile k+1's input bytes and tile
+// k+2's offsets are in flight in registers.  gfx9 counts stores in vmcnt
+// too (in issue order with loads), so tile k-1's output and lengths are
+// stored after tile k+1's loads are issued and before tile k decodes, and the
+// decode issues no global memory operation: when tile k+1 starts, everything
+// it waits for was issued a whole decode earlier.
+
+struct TileOff {  // raw loads: in_off / out_off of literals s + 2*lane + {0, 1}, and of s + tile
+  uint64_t i0, i1, o0, o1, ie, oe;
+};
 
 __device__ __forceinline__ uint32_t vzero() {
   uint32_t z;
@@ -266,73 +375,253 @@ __device__ __forceinline__ uint32_t vzero() {
   return z;
 }
 
-__device__ __forceinline__ uint64_t vload(const uint64_t *__restrict__ p, uint64_t i) { return p[i + vzero()]; }
-
 __device__ __forceinline__ uint64_t uniform64(uint64_t v) {
   return (uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)v) |
          ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32);
 }
 
-struct Next {           // raw loads for the sub-tile that starts at literal `cur`
-  uint64_t ie64, oe64;  // in_off / out_off at the end of literal cur + min(tid, cnt-1)
-  u32x4 v[kPF];         // input chunk min(tid + kT*k, chunks-1) from the 16-B aligned start
-};
-
-// Input chunks the prefetch covers for a sub-tile whose input starts at ic
-// (range input ends at iend).
-__device__ __forceinline__ uint32_t prefetch_chunks(const uint8_t *in, uint64_t in_bias, uint64_t ic, uint64_t iend) {
-  const uint32_t delta = (uint32_t)((uintptr_t)(in + (ic - in_bias)) & 15u);
-  return (uint32_t)min(((iend - ic) + delta + 15u) >> 4, (uint64_t)(kInCap / 16));
+// Offsets of the tile that starts at literal s (indices clamped to L1, so a
+// tile past the range loads the range end).
+__device__ __forceinline__ void load_off(TileOff &t, const uint64_t *__restrict__ in_off,
+                                         const uint64_t *__restrict__ out_off, uint64_t s, uint64_t L1,
+                                         uint32_t tl, uint32_t lane) {
+  const uint32_t z = vzero();  // keeps the loads per-lane vector loads
+  const uint64_t j0 = min(s + 2u * lane, L1) + z, j1 = min(s + 2u * lane + 1u, L1) + z;
+  const uint64_t je = min(s + (uint64_t)tl, L1) + z;
+  t.i0 = in_off[j0];
+  t.i1 = in_off[j1];
+  t.o0 = out_off[j0];
+  t.o1 = out_off[j1];
+  t.ie = in_off[je];
+  t.oe = out_off[je];
 }
 
-// ic: in_off[cur], iend: in_off[lim], both uniform.
-__device__ __forceinline__ void issue_next(Next &nx, const uint8_t *__restrict__ in, uint64_t in_bias,
-                                           const uint64_t *__restrict__ in_off,
-                                           const uint64_t *__restrict__ out_off, uint64_t cur, uint64_t lim,
-                                           uint64_t ic, uint64_t iend, uint32_t tid) {
-  const uint64_t j = min(cur + 1u + tid, lim);
-  nx.ie64 = in_off[j];
-  nx.oe64 = out_off[j];
-  if (!kPrefetchInput) return;
-  const uint8_t *a = in + (ic - in_bias);
-  const u32x4 *src = (const u32x4 *)(a - ((uintptr_t)a & 15u));
-  const uint32_t chunks = prefetch_chunks(in, in_bias, ic, iend);
+struct TileIn {
+  u32x4 v[kPF];
+};
+
+// Input chunks [0, kPF*64) from the 16-B aligned start of a tile whose input
+// is [ib, iend) in in_off units (chunk indices clamped; nothing for an empty
+// range, whose aligned chunk may lie past the buffer).
+__device__ __forceinline__ void load_in(TileIn &t, const uint8_t *__restrict__ in, uint64_t in_bias, uint64_t ib,
+                                        uint64_t iend, uint32_t lane) {
+  const uint8_t *a = in + (ib - in_bias);
+  const uint32_t delta = (uint32_t)((uintptr_t)a & 15u);
+  const u32x4 *src = (const u32x4 *)(a - delta);
+  const uint64_t need = ((iend - ib) + delta + 15u) >> 4;
+  const uint32_t chunks = (uint32_t)min(need, (uint64_t)(kWIn / 16));
+  if (iend == ib) return;
 #pragma unroll
   for (int k = 0; k < kPF; k++) {
-    const uint32_t c = min(tid + (uint32_t)kT * k, chunks ? chunks - 1u : 0u);
-    nx.v[k] = __builtin_nontemporal_load(src + c);  // aligned: never crosses a page
+    const uint32_t c = min(lane + (uint32_t)kWave * k, chunks - 1u);
+    t.v[k] = __builtin_nontemporal_load(src + c);  // aligned, holds a valid byte: never crosses a page
   }
 }
 
-__device__ __forceinline__ void put_in_chunk(Smem &sm, uint32_t c, u32x4 v) {
+__device__ __forceinline__ void put_chunk(WaveSmem &ws, uint32_t c, u32x4 v) {
   v.x = __builtin_bswap32(v.x);
   v.y = __builtin_bswap32(v.y);
   v.z = __builtin_bswap32(v.z);
   v.w = __builtin_bswap32(v.w);
-  *(u32x4 *)(sm.in_w + kInWords - 4u - 4u * c) = v.wzyx;
+  *(u32x4 *)(ws.in_w + 4u * c) = v;
 }
 
-// All of a thread's chunk loads are issued before the first LDS write, so the
-// staging pays one memory latency, not one per chunk.
-__device__ __forceinline__ void stage_chunks(Smem &sm, const u32x4 *src, uint32_t chunks, uint32_t tid) {
-  u32x4 v[kPF];
+// out_len / status of literals [s, s + m) from the wave's len array.
+__device__ __forceinline__ void flush_lens(const WaveSmem &ws, uint64_t s, uint32_t m, uint32_t *__restrict__ out_len,
+                                           uint8_t *__restrict__ status, uint32_t lane) {
 #pragma unroll
-  for (int k = 0; k < kPF; k++) {
-    const uint32_t c = tid + (uint32_t)kT * k;
-    if (c < chunks) v[k] = __builtin_nontemporal_load(src + c);  // aligned: never crosses a page
-  }
-#pragma unroll
-  for (int k = 0; k < kPF; k++) {
-    const uint32_t c = tid + (uint32_t)kT * k;
-    if (c < chunks) put_in_chunk(sm, c, v[k]);
+  for (int h = 0; h < 2; h++) {
+    const uint32_t j = lane + (uint32_t)kWave * h;
+    if (j < m) {
+      const uint32_t v = ws.len[j];
+      out_len[s + j] = v & 0x7fffffffu;
+      status[s + j] = (uint8_t)(v >> 31);
+    }
   }
 }
 
-__global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu((kT / 64 * MHQ_DEC_BLOCKS + 3) / 4))) void decode_kernel(
-    const uint8_t *__restrict__ in, const uint64_t *__restrict__ in_off, uint64_t in_bias, uint64_t n,
-    uint8_t *__restrict__ out, const uint64_t *__restrict__ out_off, uint64_t out_bias,
-    uint32_t *__restrict__ out_len, uint8_t *__restrict__ status, const uint32_t *__restrict__ g_lut1,
-    const uint16_t *__restrict__ g_lut2, uint64_t per_block) {
+// Decodes the m literals whose boundary records rec[0..m] and input bytes are
+// staged: zero the output region, sort, decode into out_w / len.
+__device__ __forceinline__ void decode_piece(const Smem &sm, WaveSmem &ws, uint32_t m, uint32_t out_bytes,
+                                             uint32_t lane) {
+  for (uint32_t c = lane; c < (out_bytes + 15u) >> 4; c += kWave) *(u32x4 *)(ws.out_w + 4u * c) = u32x4{0u, 0u, 0u, 0u};
+  // counting sort by encoded length, longest first
+  ws.hist[lane] = 0;
+  wave_sync();
+  uint32_t key[2], rk[2];
+#pragma unroll
+  for (int h = 0; h < 2; h++) {
+    const uint32_t j = lane + (uint32_t)kWave * h;
+    key[h] = 0;
+    rk[h] = 0;
+    if (j < m) {
+      const uint32_t bytes = (ws.rec[j + 1] & 0xffffu) - (ws.rec[j] & 0xffffu);
+      const uint32_t bk = bytes < 48u ? bytes : min(48u + ((bytes - 48u) >> 3), (uint32_t)kBuckets - 1u);
+      key[h] = (uint32_t)kBuckets - 1u - bk;
+      rk[h] = atomicAdd(&ws.hist[key[h]], 1u);
+    }
+  }
+  wave_sync();
+  {
+    const uint32_t hcount = ws.hist[lane];
+    uint32_t x = hcount;
+#pragma unroll
+    for (int d = 1; d < kWave; d <<= 1) {
+      const uint32_t y = __shfl_up(x, d);
+      if ((int)lane >= d) x += y;
+    }
+    wave_sync();
+    ws.hist[lane] = x - hcount;
+  }
+  wave_sync();
+#pragma unroll
+  for (int h = 0; h < 2; h++) {
+    const uint32_t j = lane + (uint32_t)kWave * h;
+    if (j < m) ws.order[ws.hist[key[h]] + rk[h]] = (uint8_t)j;
+  }
+  wave_sync();
+  // Lane t decodes rank t, then rank 127 - t if there is one: the 64 longest
+  // literals one per lane, the rest on the lanes with the shortest of those
+  // (LPT).  The lane's two fast loops run back to back in one loop (it moves
+  // to its second literal in place), so lanes stay busy until all are done;
+  // the short checked tails follow, one literal at a time.
+#ifdef MHQ_X_NODEC  // timing experiment only: sort and zero, no decode
+  if (lane < m) ws.len[lane] = 0;
+  wave_sync();
+  return;
+#endif
+  const bool hasA = lane < m, hasB = 2u * kWave - 1u - lane < m;
+  LitRef A, B;
+  A.load(ws, hasA ? ws.order[lane] : 0u);
+  B.load(ws, hasB ? ws.order[2u * kWave - 1u - lane] : 0u);
+  const uint32_t ostartA = A.optr, ostartB = B.optr;
+  const bool roomA = hasA && A.roomy(), roomB = hasB && B.roomy();
+  const bool fastA = roomA && A.p + 24u <= A.endbit, fastB = roomB && B.p + 24u <= B.endbit;
+  uint32_t sA = 0, sB = 0;  // 1 | status << 1 once the fast loop has finished the literal
+  {
+    const LitRef &C = fastA ? A : B;
+    BitBuf in, inB;  // inB: B's stream, set up once for the in-loop switch
+    in.init(ws.in_w, C.p);
+    inB.init(ws.in_w, B.p);
+    OutAcc out;
+    out.init(C.optr);
+    uint32_t endbit = C.endbit, bad = 0;
+    int lim = (int)endbit - 24;
+    bool onB = !fastA, active = fastA || fastB;
+    // One loop with a single latch: a lane that finishes its first literal's
+    // fast part moves on to its second at once (a loop with a separate
+    // "switch" back edge is restructured into nested loops that run every
+    // lane's first literal to the end before any second one starts).
+    while (active) {
+#ifdef MHQ_DIAG_COUNT  // diagnostic build: fast-loop wave iterations and active lanes
+      {
+        const uint64_t mask = __ballot(1);
+        if (lane == (uint32_t)__builtin_ctzll(mask)) {
+          atomicAdd(&g_cnt[0], 1ull);
+          atomicAdd(&g_cnt[1], (unsigned long long)__popcll(mask));
+        }
+      }
+#endif
+      fast_step(sm, ws, in, out, endbit, lim, bad);
+      if ((int)in.p > lim) {  // this literal's fast part is over (lim = -1: the literal is finished)
+        atomicOr(&ws.out_w[out.ow], (uint32_t)out.acc);  // bits of a completed word not yet written
+        const uint32_t st = lim < 0 ? 1u | (bad << 1) : 0u;
+        if (onB) {
+          B.p = in.p;
+          B.optr = out.optr();
+          sB = st;
+        } else {
+          A.p = in.p;
+          A.optr = out.optr();
+          sA = st;
+        }
+        active = !onB && fastB;
+        in = inB;  // (unused unless active)
+        out.init(B.optr);
+        endbit = B.endbit;
+        lim = (int)endbit - 24;
+        bad = 0;
+        onB = true;
+      }
+    }
+  }
+#ifdef MHQ_X_NOTAIL  // timing experiment only: no literal ends
+  sA |= 1u;
+  sB |= 1u;
+#endif
+  if (hasA) {
+    ws.len[A.lit] = (sA & 1u) ? (A.optr - ostartA) | ((sA >> 1) << 31)
+                    : roomA   ? decode_end(sm, ws, A.p, A.endbit, A.optr, ostartA)
+                              : decode_checked(sm, ws, A.p, A.endbit, A.optr, A.oend);
+  }
+  if (hasB) {
+    ws.len[B.lit] = (sB & 1u) ? (B.optr - ostartB) | ((sB >> 1) << 31)
+                    : roomB   ? decode_end(sm, ws, B.p, B.endbit, B.optr, ostartB)
+                              : decode_checked(sm, ws, B.p, B.endbit, B.optr, B.oend);
+  }
+  wave_sync();
+}
+
+// Slow path: a tile whose bytes exceed the slices, in greedy pieces staged
+// synchronously from global memory; a literal larger than a slice alone is
+// decoded by lane 0 from global memory.
+__device__ void decode_tile_pieces(const Smem &sm, WaveSmem &ws, const uint8_t *__restrict__ in,
+                                   const uint64_t *__restrict__ in_off, uint64_t in_bias, uint8_t *__restrict__ out,
+                                   const uint64_t *__restrict__ out_off, uint64_t out_bias,
+                                   uint32_t *__restrict__ out_len, uint8_t *__restrict__ status, uint64_t s,
+                                   uint32_t cnt, uint32_t lane) {
+  uint32_t cur = 0;
+  while (cur < cnt) {
+    const uint64_t ib = uniform64(in_off[s + cur + vzero()]), ob = uniform64(out_off[s + cur + vzero()]);
+    const uint8_t *ia = in + (ib - in_bias);
+    uint8_t *oa = out + (ob - out_bias);
+    const uint32_t idelta = (uint32_t)((uintptr_t)ia & 15u), odelta = (uint32_t)((uintptr_t)oa & 15u);
+    // longest prefix [cur, cur + m) that fits both slices (the test is monotone
+    // in the literal index, so the count of fitting literals is that length)
+    uint32_t m = 0;
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+      const uint32_t j = cur + lane + (uint32_t)kWave * h;  // literal j ends at offset index j + 1
+      const bool ok = j < cnt && (in_off[s + j + 1] - ib) + idelta <= (uint64_t)kWIn &&
+                      (out_off[s + j + 1] - ob) + odelta <= (uint64_t)kWOut;
+      m += popc64(__ballot(ok));
+    }
+    if (m == 0) {
+      if (lane == 0) {
+        const uint64_t ie = in_off[s + cur + 1], oe = out_off[s + cur + 1];
+        decode_literal_global(ia, ie - ib, oa, oe - ob, sm, out_len + s + cur, status + s + cur);
+      }
+      cur += 1;
+      continue;
+    }
+#pragma unroll
+    for (int h = 0; h < 3; h++) {
+      const uint32_t j = lane + (uint32_t)kWave * h;
+      if (j <= m) {
+        const uint64_t ij = in_off[s + cur + j], oj = out_off[s + cur + j];
+        ws.rec[j] = (uint32_t)(ij - ib + idelta) | (uint32_t)(oj - ob + odelta) << 16;
+      }
+    }
+    wave_sync();
+    const uint32_t in_bytes = ws.rec[m] & 0xffffu, out_bytes = ws.rec[m] >> 16;
+    stage_in<true, false>(ws.in_w, kWIn / 4, ia - idelta, in_bytes, lane);
+    wave_sync();
+    decode_piece(sm, ws, m, out_bytes, lane);
+    store_out(oa - odelta, (const uint8_t *)ws.out_w, odelta, out_bytes, lane);
+    flush_lens(ws, s + cur, m, out_len, status, lane);
+    wave_sync();
+    cur += m;
+  }
+}
+
+__global__ __launch_bounds__(kT) void decode_kernel(const uint8_t *__restrict__ in, const uint64_t *__restrict__ in_off,
+                                                    uint64_t in_bias, uint64_t n, uint8_t *__restrict__ out,
+                                                    const uint64_t *__restrict__ out_off, uint64_t out_bias,
+                                                    uint32_t *__restrict__ out_len, uint8_t *__restrict__ status,
+                                                    const uint32_t *__restrict__ g_lut1,
+                                                    const uint16_t *__restrict__ g_lut2,
+                                                    const uint8_t *__restrict__ g_len, uint64_t per_block,
+                                                    uint32_t tl) {
   __shared__ Smem sm;
   const uint32_t tid = threadIdx.x;
   const uint32_t lane = tid % kWave;
@@ -340,133 +629,105 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu((kT / 64 * M
   const uint64_t L0 = (uint64_t)blockIdx.x * per_block;
   if (L0 >= n) return;
   const uint64_t L1 = min(L0 + per_block, n);
-  uint64_t cur = L0;
-  uint64_t i_cur = uniform64(vload(in_off, L0)), o_cur = uniform64(vload(out_off, L0));
-  const uint64_t i_end = uniform64(vload(in_off, L1));
-  Next nx;
-  issue_next(nx, in, in_bias, in_off, out_off, cur, L1, i_cur, i_end, tid);
+  const uint32_t ntiles = (uint32_t)((L1 - L0 + tl - 1) / tl);
+  WaveSmem &ws = sm.w[wave];
+  TL(0);
+
+  // Workgroup b owns literals [L0, L1), in tiles of tl literals.  Wave w takes
+  // tiles w, w + kWaves, w + 2 kWaves, then claims from the LDS counter, three
+  // tiles ahead of the one it decodes.
+  uint32_t tile = wave, tile2 = tile + kWaves, tile3 = tile + 2 * kWaves;
+  TileOff off, off2;
+  load_off(off, in_off, out_off, L0 + (uint64_t)tile * tl, L1, tl, lane);
+  load_off(off2, in_off, out_off, L0 + (uint64_t)tile2 * tl, L1, tl, lane);
   for (uint32_t i = tid; i < kLut1Size / 4; i += kT) ((u32x4 *)sm.lut1)[i] = ((const u32x4 *)g_lut1)[i];
   for (uint32_t i = tid; i < kLut2Size / 8; i += kT) ((u32x4 *)sm.lut2)[i] = ((const u32x4 *)g_lut2)[i];
-  uint8_t *pd_o = nullptr;  // the previous sub-tile's output, still in LDS
-  uint32_t pd_lo = 0, pd_hi = 0;
-  bool pending = false;
-#ifdef MHQ_DIAG_STAMPS
-  unsigned long long ph[7] = {0, 0, 0, 0, 0, 0, 0};
-  unsigned long long t_last = stamp_now();
-#endif
+  if (tid < 64) ((uint32_t *)sm.clen)[tid] = ((const uint32_t *)g_len)[tid];
+  if (tid == 0) sm.next_tile = 3 * kWaves;
+  TileIn tin;
+  load_in(tin, in, in_bias, uniform64(__shfl(off.i0, 0)), uniform64(off.ie), lane);
+  __syncthreads();
+  uint64_t pd_s = 0;  // the previous tile, still in the output slice: literals, output range
+  uint32_t pd_m = 0, pd_lo = 0, pd_hi = 0;
+  uint8_t *pd_o = nullptr;
+  [[maybe_unused]] uint32_t tl_j = 0;
 
-  while (cur < L1) {
-    // consume the prefetch (the previous sub-tile's decode ended with a barrier: in_w is free)
-    const uint32_t cnt = (uint32_t)min((uint64_t)kT, L1 - cur);
-    const uint32_t ie = (uint32_t)(nx.ie64 - i_cur), oe = (uint32_t)(nx.oe64 - o_cur);  // end of literal cur+tid
-    const uint8_t *ia = in + (i_cur - in_bias);
-    uint8_t *oa = out + (o_cur - out_bias);
-    const uint32_t idelta = (uint32_t)((uintptr_t)ia & 15u);
-    const uint32_t odelta = (uint32_t)((uintptr_t)oa & 15u);
-    if (kPrefetchInput) {
-      const uint32_t chunks = prefetch_chunks(in, in_bias, i_cur, i_end);
+  while (tile < ntiles) {
+    const uint64_t s = L0 + (uint64_t)tile * tl;
+    const uint32_t cnt = (uint32_t)min((uint64_t)tl, L1 - s);
+    const uint64_t ib = uniform64(__shfl(off.i0, 0)), ob = uniform64(__shfl(off.o0, 0));
+    const uint64_t ie = uniform64(off.ie), oe = uniform64(off.oe);
+    const uint8_t *ia = in + (ib - in_bias);
+    uint8_t *oa = out + (ob - out_bias);
+    const uint32_t idelta = (uint32_t)((uintptr_t)ia & 15u), odelta = (uint32_t)((uintptr_t)oa & 15u);
+    const bool fits = (ie - ib) + idelta <= (uint64_t)kWIn && (oe - ob) + odelta <= (uint64_t)kWOut;
+    // claim the tile three ahead (used when this one is done)
+    uint32_t tile4 = 0;
+    if (lane == 0) tile4 = atomicAdd(&sm.next_tile, 1u);
+    if (fits) {  // stage this tile: input words, boundary records
+      const uint32_t chunks = (uint32_t)(((ie - ib) + idelta + 15u) >> 4);
 #pragma unroll
       for (int k = 0; k < kPF; k++) {
-        const uint32_t c = tid + (uint32_t)kT * k;
-        if (c < chunks) put_in_chunk(sm, c, nx.v[k]);
+        const uint32_t c = lane + (uint32_t)kWave * k;
+        if (c < chunks) put_chunk(ws, c, tin.v[k]);
       }
+      const uint32_t j0 = 2u * lane;
+      if (j0 < cnt) ws.rec[j0] = (uint32_t)(off.i0 - ib + idelta) | (uint32_t)(off.o0 - ob + odelta) << 16;
+      if (j0 + 1u < cnt) ws.rec[j0 + 1] = (uint32_t)(off.i1 - ib + idelta) | (uint32_t)(off.o1 - ob + odelta) << 16;
+      if (lane == 0) ws.rec[cnt] = (uint32_t)(ie - ib + idelta) | (uint32_t)(oe - ob + odelta) << 16;
     }
-    // the sub-tile: literals cur + [0, m) fit both slices
-    const bool fits = tid < cnt && ie + idelta <= (uint32_t)kInCap && oe + odelta <= (uint32_t)kOutCap;
-    uint32_t m = (uint32_t)__syncthreads_count(fits);
-    const bool oversized = m == 0;  // literal `cur` alone is larger than a slice
-    m = oversized ? 1u : m;
-    STAMP(0);
-    if (tid == m - 1u) {
-      sm.nbase[0] = nx.ie64;
-      sm.nbase[1] = nx.oe64;
+    // the next tile's input (its offsets arrived during the previous decode), the offsets of the one after
+    load_in(tin, in, in_bias, uniform64(__shfl(off2.i0, 0)), uniform64(off2.ie), lane);
+    off = off2;
+    load_off(off2, in_off, out_off, L0 + (uint64_t)tile3 * tl, L1, tl, lane);
+    TL(1 + 3 * tl_j);
+    // the previous tile's output and lengths leave, then this tile decodes
+    if (pd_o) {
+      store_out(pd_o, (const uint8_t *)ws.out_w, pd_lo, pd_hi, lane);
+      flush_lens(ws, pd_s, pd_m, out_len, status, lane);
     }
-    if (tid == 0) sm.rec[0] = idelta | odelta << 16;
-    if (fits) sm.rec[tid + 1] = (ie + idelta) | (oe + odelta) << 16;
-    if (tid < kBuckets) sm.hist[tid] = 0;
-    __syncthreads();
-    // start loading the next sub-tile, then let the previous one's output go
-    const uint64_t i_nxt = sm.nbase[0], o_nxt = sm.nbase[1];
-    issue_next(nx, in, in_bias, in_off, out_off, cur + m, L1, i_nxt, i_end, tid);
-    if (pending) store_out(pd_o, (const uint8_t *)sm.out_w, pd_lo, pd_hi, tid, kT);
-    pending = false;
-    if (oversized) {
-      if (tid == 0)
-        decode_literal_global(ia, i_nxt - i_cur, oa, o_nxt - o_cur, sm.lut1, sm.lut2, out_len + cur, status + cur);
-    } else {
-      const uint32_t in_bytes = sm.rec[m] & 0xffffu, out_bytes = sm.rec[m] >> 16;
-      __syncthreads();  // out_w has been read by the flush
-      if (!kPrefetchInput) stage_chunks(sm, (const u32x4 *)(ia - idelta), (in_bytes + 15u) >> 4, tid);
-      for (uint32_t c = tid; c < (out_bytes + 15u) >> 4; c += kT) *(u32x4 *)(sm.out_w + 4u * c) = u32x4{0u, 0u, 0u, 0u};
-      STAMP(1);
-#ifdef MHQ_DEC_NOSORT
-      __syncthreads();
-      const uint32_t lit = tid;
-#else
-      // counting sort by encoded length: the thread of rank r decodes literal order[r]
-      uint32_t bk = 0, rk = 0;
-      if (tid < m) {
-        const uint32_t bytes = (sm.rec[tid + 1] & 0xffffu) - (sm.rec[tid] & 0xffffu);
-        bk = bytes < 48u ? bytes : min(48u + ((bytes - 48u) >> 3), (uint32_t)kBuckets - 1u);
-        rk = atomicAdd(&sm.hist[bk], 1u);
-      }
-      __syncthreads();
-      if (wave == 0) {  // exclusive scan of the bucket counts
-        const uint32_t h = sm.hist[lane];
-        uint32_t x = h;
-#pragma unroll
-        for (int d = 1; d < kWave; d <<= 1) {
-          const uint32_t y = __shfl_up(x, d);
-          if ((int)lane >= d) x += y;
-        }
-        sm.hist[lane] = x - h;
-      }
-      __syncthreads();
-      if (tid < m) sm.order[sm.hist[bk] + rk] = (uint16_t)tid;
-      __syncthreads();
-      const uint32_t lit = tid < m ? sm.order[tid] : 0u;
-#endif
-      STAMP(2);
-      if (tid < m) {
-        const uint32_t r0 = sm.rec[lit], r1 = sm.rec[lit + 1];
-#ifdef MHQ_DIAG_NO_DECODE  // diagnostic build: staging and stores only
-        const uint32_t v = 0;
-#else
-        const uint32_t v = decode_one(sm, (r0 & 0xffffu) * 8u, (r1 & 0xffffu) * 8u, r0 >> 16, r1 >> 16);
-#endif
-        out_len[cur + lit] = v & 0x7fffffffu;
-        status[cur + lit] = (uint8_t)(v >> 31);
-      }
-      STAMP(3);
-      __syncthreads();  // decode done: in_w free, out_w complete
+    pd_o = nullptr;
+    wave_sync();
+    TL(2 + 3 * tl_j);
+    if (fits) {
+      const uint32_t out_bytes = ws.rec[cnt] >> 16;
+      decode_piece(sm, ws, cnt, out_bytes, lane);
       pd_o = oa - odelta;
       pd_lo = odelta;
       pd_hi = out_bytes;
-      pending = true;
-#ifdef MHQ_DIAG_STAMPS
-      ph[6]++;
-#endif
+      pd_s = s;
+      pd_m = cnt;
+    } else {
+      decode_tile_pieces(sm, ws, in, in_off, in_bias, out, out_off, out_bias, out_len, status, s, cnt, lane);
     }
-    cur += m;
-    i_cur = i_nxt;
-    o_cur = o_nxt;
+    TL(3 + 3 * tl_j);
+    tl_j++;
+    tile = tile2;
+    tile2 = tile3;
+    tile3 = __builtin_amdgcn_readfirstlane(tile4);
   }
-  if (pending) store_out(pd_o, (const uint8_t *)sm.out_w, pd_lo, pd_hi, tid, kT);
-#ifdef MHQ_DIAG_STAMPS
-  if (lane == 0)
-    for (int i = 0; i < 7; i++) atomicAdd(&g_diag[i], ph[i]);
-#endif
+  if (pd_o) {
+    store_out(pd_o, (const uint8_t *)ws.out_w, pd_lo, pd_hi, lane);
+    flush_lens(ws, pd_s, pd_m, out_len, status, lane);
+  }
+  TL(63);
 }
 
 }  // namespace
 
-#ifdef MHQ_DIAG_STAMPS
+#ifdef MHQ_DIAG_COUNT
 extern "C" int mhq_diag_read(unsigned long long *out, int n) {
   unsigned long long h[8];
-  if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_diag), sizeof(h)) != hipSuccess) return -1;
+  if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_cnt), sizeof(h)) != hipSuccess) return -1;
   for (int i = 0; i < n && i < 8; i++) out[i] = h[i];
   unsigned long long z[8] = {0};
-  return hipMemcpyToSymbol(HIP_SYMBOL(g_diag), z, sizeof(z)) == hipSuccess ? 0 : -1;
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_cnt), z, sizeof(z)) == hipSuccess ? 0 : -1;
+}
+#endif
+#ifdef MHQ_DIAG_TIMELINE
+extern "C" int mhq_diag_timeline(unsigned long long *out, int n) {
+  const int m = n < 1024 * 16 * kTlSlots ? n : 1024 * 16 * kTlSlots;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_tl), m * sizeof(unsigned long long)) == hipSuccess ? kTlSlots : -1;
 }
 #endif
 
@@ -474,10 +735,17 @@ hipError_t launch_decode(const DevTables &t, const uint8_t *in, const uint64_t *
                          uint64_t n, uint8_t *out, const uint64_t *out_off, uint64_t out_bias,
                          uint32_t *out_len, uint8_t *status, hipStream_t s) {
   if (n == 0) return hipSuccess;
-  const unsigned grid = dev::tile_grid((n + kT - 1) / kT, 1, MHQ_DEC_BLOCKS * MHQ_PER_CU);
-  const uint64_t per_block = (n + grid - 1) / grid;
+  // One workgroup per CU, each a contiguous range of whole wave tiles.  The
+  // tile length (<= kTile) is chosen so that every wave gets the same number
+  // of tiles: no wave idles through a last, partial round.
+  const uint64_t cus = (uint64_t)dev::device_cus();
+  const uint64_t slots = cus * kWaves;
+  const uint64_t rounds = (n + slots * kTile - 1) / (slots * kTile);
+  const uint64_t tl = std::max<uint64_t>(1, (n + slots * rounds - 1) / (slots * rounds));
+  const uint64_t per_block = (((n + cus - 1) / cus + tl - 1) / tl) * tl;
+  const unsigned grid = (unsigned)((n + per_block - 1) / per_block);
   decode_kernel<<<dim3(grid), dim3(kT), 0, s>>>(in, in_off, in_bias, n, out, out_off, out_bias, out_len, status,
-                                                 t.lut1, t.lut2, per_block);
+                                                 t.lut1, t.lut2, t.len, per_block, (uint32_t)tl);
   return hipGetLastError();
 }
 

@@ -46,7 +46,7 @@ bool build_tables(Tables *t) {
     int l0 = 0;
     int s0 = match_code(*t, idx, kLut1Bits, &l0);
     if (s0 < 0) {
-      t->lut1[idx] = lut1_entry(0, 0, 0, 0, 0);
+      t->lut1[idx] = lut1_entry(0, 0, 0, 0);
       continue;
     }
     int rest = kLut1Bits - l0;
@@ -54,9 +54,9 @@ bool build_tables(Tables *t) {
     int l1 = 0;
     int s1 = rest > 0 ? match_code(*t, wrest, rest, &l1) : -1;
     if (s1 >= 0)
-      t->lut1[idx] = lut1_entry((uint32_t)s0, (uint32_t)s1, (uint32_t)l0, (uint32_t)(l0 + l1), 2);
+      t->lut1[idx] = lut1_entry((uint32_t)s0, (uint32_t)s1, (uint32_t)(l0 + l1), 2);
     else
-      t->lut1[idx] = lut1_entry((uint32_t)s0, 0, (uint32_t)l0, (uint32_t)l0, 1);
+      t->lut1[idx] = lut1_entry((uint32_t)s0, 0, (uint32_t)l0, 1);
   }
 
   // LUT2: codes longer than 12 bits, keyed by their count of leading ones

@@ -17,11 +17,14 @@ constexpr int kLut2SubBits = 5;               // bits after the first 0 of a lon
 constexpr int kLut2Size = 32 << kLut2SubBits; // [leading ones 0..31][5 bits] x u16
 constexpr int kEosOnes = 30;                  // all-ones prefix where EOS would be
 
-// LUT1 entry layout (u32):
-//   [7:0] sym0  [15:8] sym1  [20:16] len0  [25:21] total bits  [27:26] nsym
-// nsym == 0: the first code is longer than 12 bits -> LUT2 path.
-constexpr uint32_t lut1_entry(uint32_t s0, uint32_t s1, uint32_t l0, uint32_t tot, uint32_t ns) {
-  return s0 | (s1 << 8) | (l0 << 16) | (tot << 21) | (ns << 26);
+// LUT1 entry layout (u32), one field per byte so the decode loop can use
+// each field straight from the entry (a 64-bit shift takes its count from
+// bits [5:0]; SDWA operands select a byte or half-word):
+//   [7:0] total bits  [15:8] 8 * nsym  [23:16] sym0  [31:24] sym1 (0 for one-symbol entries)
+// An entry of 0: the first code is longer than 12 bits (or is the all-ones EOS
+// prefix) -> LUT2 path.
+constexpr uint32_t lut1_entry(uint32_t s0, uint32_t s1, uint32_t tot, uint32_t ns) {
+  return ns ? (tot | ((ns * 8u) << 8) | (s0 << 16) | (s1 << 24)) : 0u;
 }
 // LUT2 entry layout (u16): [7:0] sym  [12:8] len (0 = no code).
 

@@ -36,6 +36,36 @@ def batch_for(name: str, n: int):
     raise SystemExit(f"unknown config {name}")
 
 
+def timeline_report(fn):
+    """Summarises the MHQ_DIAG_TIMELINE build's per-wave stamps (last launch):
+    slot 0 start, 63 end, tile j: 1+3j+k, k = 0 next loads issued, 1 previous
+    output flushed, 2 decoded."""
+    import ctypes
+
+    W, S = 1024 * 16, 64
+    buf = (ctypes.c_ulonglong * (W * S))()
+    fn(buf, W * S)
+    a = np.frombuffer(buf, dtype=np.uint64).reshape(W, S).astype(np.int64)
+    a = a[a[:, 0] > 0]
+    t0 = a[:, 0].min()
+    us = lambda x: (x - t0) / 100.0  # 100 MHz ticks -> us
+    end = us(a[:, S - 1])
+    print(f"timeline: {a.shape[0]} waves, start spread {us(a[:, 0]).max():.2f} us, end max {end.max():.2f} "
+          f"p50 {np.percentile(end, 50):.2f} p10 {np.percentile(end, 10):.2f} us", file=sys.stderr)
+    prev = a[:, 0]
+    for j in range(20):
+        b = 1 + 3 * j
+        ok = a[:, b + 2] > 0
+        if not ok.any():
+            break
+        x = a[ok]
+        pv = prev[ok]
+        print(f"  tile {j}: waves={ok.sum()} stage {(x[:, b] - pv).mean() / 100:.2f} flush {(x[:, b + 1] - x[:, b]).mean() / 100:.2f} "
+              f"decode {(x[:, b + 2] - x[:, b + 1]).mean() / 100:.2f} (p90 {np.percentile(x[:, b + 2] - x[:, b + 1], 90) / 100:.2f}) "
+              f"done@{us(x[:, b + 2]).mean():.2f}", file=sys.stderr)
+        prev = np.where(a[:, b + 2] > 0, a[:, b + 2], prev)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--kernel", default="decode", choices=["decode", "encode", "encode_len", "offsets"])
@@ -120,12 +150,12 @@ def main():
     ms = e0.elapsed_time(e1) / args.iters
     if diag:
         diag(buf, 8)
-        names = ["top_fit", "rec_stage", "sort", "decode", "-", "-"]
-        tot = sum(buf[:6]) or 1
-        print("diag phases (share of wave cycles): " + " ".join(
-            f"{nm}={buf[i] / tot:.3f}" for i, nm in enumerate(names)),
-            f"wave-cycles/launch={tot / args.iters:.3g} sub-tiles/launch={buf[6] / args.iters:.4g}"
-            f" decode-cycles/sub-tile/wave={buf[3] / max(buf[6], 1):.1f}", file=sys.stderr)
+        it, lanes = buf[0] / args.iters, buf[1] / args.iters
+        print(f"diag counts per launch: fast-loop wave iterations {it:.4g}, active lanes {lanes:.4g} "
+              f"(utilisation {lanes / max(it * 64, 1):.3f}), per literal {lanes / n:.2f} lane-steps", file=sys.stderr)
+    tl = getattr(_lib.load(), "mhq_diag_timeline", None)
+    if tl:
+        timeline_report(tl)
     if args.kernel == "decode" and not args.no_check:
         s = slots[0]
         assert int(s["st"].sum().item()) == 0

@@ -1,0 +1,10 @@
+#!/bin/bash
+# Quick GPU iteration: parity tests, decode timings on the headline batches, timeline build.
+set -o pipefail
+mkdir -p gpurun_out
+timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1
+rc=$?; tail -5 gpurun_out/pytest_gpu.log; [ $rc -eq 0 ] || exit $rc
+for cfg in northstar config2; do
+  timeout -k 10 120 python3 tools/kernel_driver.py --kernel decode --config $cfg --iters 30 2>/dev/null || exit 1
+done
+bash tools/diag_timeline.sh
