@@ -107,6 +107,58 @@ int mhq_huff_decode_dev(mhq_ctx *ctx, int dev, const uint8_t *in, const uint64_t
                         uint8_t *out, const uint64_t *out_off, uint32_t *out_len, uint8_t *status,
                         void *stream);
 
+/* ---------------- string literals: H bit + prefix integer + payload --------
+ * Batch Reader.ReadString(prefix) and Writer.WriteStringRaw(s, prefix, choice)
+ * (hc/io.go:73-97, 153-197) with the prefix integers of Reader.ReadInt /
+ * Writer.WriteInt (hc/io.go:25-55, 110-137).  A string literal starts on an
+ * octet whose low prefix+1 bits hold the H bit and the length prefix; the bits
+ * above belong to the caller's opcode (HPACK: prefix 7; QPACK: 7/5/3 after
+ * 1/3/5-bit opcodes, hc/qpackdecoder.go:127,163,340). */
+
+/* Per-string outcome of a read (status[]), in ReadString's terms. */
+#define MHQ_STR_OK 0      /* (string, nil); also ("", nil) when the H bit or the length cannot be read */
+#define MHQ_STR_INVALID 1 /* ("", "invalid Huffman coding") */
+#define MHQ_STR_EOF 2     /* ("", io.EOF): nothing decoded from a Huffman literal, or a raw one cut to 0 bytes */
+#define MHQ_STR_NOSPACE 3 /* the output buffer could not hold this string (not a reference outcome) */
+
+/* HuffmanCodingChoice (hc/io.go:140-150). */
+#define MHQ_HUFF_AUTO 0   /* Huffman iff strictly shorter (hc/io.go:172) */
+#define MHQ_HUFF_ALWAYS 1
+#define MHQ_HUFF_NEVER 2
+
+/* Reads n string literals from blk[0..blk_len): literal i starts at byte
+ * pos[i] (its H bit is bit 7-prefix[i] of that octet) and may use bytes up to
+ * limit[i] (the end of its header block: the LimitedReader's underlying EOF
+ * truncates the payload silently).  The call writes out_off[0..n] (string i is
+ * out[out_off[i] .. out_off[i]+out_len[i]), regions back to back in string
+ * order), out_len[i], status[i] and next[i] (the byte after the payload).
+ * out_cap must be at least blk_len*8/5 + 1 (enough for any set of
+ * non-overlapping literals).  Device pointers; asynchronous on `stream`. */
+int mhq_read_strings_dev(mhq_ctx *ctx, int dev, const uint8_t *blk, uint64_t blk_len, const uint64_t *pos,
+                         const uint64_t *limit, const uint8_t *prefix, uint64_t n, uint8_t *out, uint64_t out_cap,
+                         uint64_t *out_off, uint32_t *out_len, uint8_t *status, uint64_t *next, void *stream);
+
+/* Frames n strings (string i is in[in_off[i]..in_off[i+1])) as
+ * WriteStringRaw(s, prefix[i], choice) after opcode bits lead[i] (the
+ * 7-prefix[i] bits above the H bit).  Writes out_off[0..n] (frame i is
+ * out[out_off[i]..out_off[i+1])) and, when out is not NULL, the frames and
+ * status[i] (MHQ_STR_OK, or MHQ_STR_NOSPACE past out_cap).  With out NULL only
+ * out_off is computed (size query).  Synchronises `stream` once (to size the
+ * Huffman scratch).  Device pointers. */
+int mhq_write_strings_dev(mhq_ctx *ctx, int dev, const uint8_t *in, const uint64_t *in_off, uint64_t n,
+                          const uint8_t *prefix, const uint8_t *lead, int choice, uint8_t *out, uint64_t out_cap,
+                          uint64_t *out_off, uint8_t *status, void *stream);
+
+/* Host-memory forms of the two calls above (device 0 of the context,
+ * synchronous).  Same arguments and layout, host pointers; out_off is written
+ * by the call. */
+int mhq_read_strings(mhq_ctx *ctx, const uint8_t *blk, uint64_t blk_len, const uint64_t *pos, const uint64_t *limit,
+                     const uint8_t *prefix, uint64_t n, uint8_t *out, uint64_t out_cap, uint64_t *out_off,
+                     uint32_t *out_len, uint8_t *status, uint64_t *next);
+int mhq_write_strings(mhq_ctx *ctx, const uint8_t *in, const uint64_t *in_off, uint64_t n, const uint8_t *prefix,
+                      const uint8_t *lead, int choice, uint8_t *out, uint64_t out_cap, uint64_t *out_off,
+                      uint8_t *status);
+
 #ifdef __cplusplus
 }
 #endif

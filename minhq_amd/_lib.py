@@ -19,6 +19,10 @@ MHQ_ENODEV = -19
 MHQ_EHIP = -1000
 MHQ_LIT_OK = 0
 MHQ_LIT_INVALID = 1
+MHQ_STR_OK = 0
+MHQ_STR_INVALID = 1
+MHQ_STR_EOF = 2
+MHQ_STR_NOSPACE = 3
 
 u8p = C.POINTER(C.c_uint8)
 u32p = C.POINTER(C.c_uint32)
@@ -41,6 +45,14 @@ SIGNATURES = {
     "mhq_huff_capacity_dev": (C.c_int, [vp, C.c_int, vp, C.c_uint64, C.c_uint64, vp, vp]),
     "mhq_huff_encode_dev": (C.c_int, [vp, C.c_int, vp, vp, C.c_uint64, vp, vp, vp]),
     "mhq_huff_decode_dev": (C.c_int, [vp, C.c_int, vp, vp, C.c_uint64, vp, vp, vp, vp, vp]),
+    "mhq_read_strings_dev": (C.c_int, [vp, C.c_int, vp, C.c_uint64, vp, vp, vp, C.c_uint64, vp, C.c_uint64,
+                                       vp, vp, vp, vp, vp]),
+    "mhq_write_strings_dev": (C.c_int, [vp, C.c_int, vp, vp, C.c_uint64, vp, vp, C.c_int, vp, C.c_uint64,
+                                        vp, vp, vp]),
+    "mhq_read_strings": (C.c_int, [vp, u8p, C.c_uint64, u64p, u64p, u8p, C.c_uint64, u8p, C.c_uint64, u64p,
+                                   u32p, u8p, u64p]),
+    "mhq_write_strings": (C.c_int, [vp, u8p, u64p, C.c_uint64, u8p, u8p, C.c_int, u8p, C.c_uint64, u64p,
+                                    u8p]),
 }
 
 _lib = None

@@ -4,6 +4,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "../../include/mhq_huff.h"
+
 namespace mhq {
 
 // Device copies of the tables built by build_tables() (huff_table.h).
@@ -30,6 +32,14 @@ hipError_t launch_offsets(const uint32_t *enc_len, uint64_t n, uint64_t base, ui
                           uint64_t *cap_off, hipStream_t s);
 // cap_off[i] = base + sum_{j<i} floor(8*(in_off[j+1]-in_off[j])/5): decode capacities
 // for a batch whose encoded offsets are known.
+// Batch ReadString / WriteStringRaw (str_frame.hip); see include/mhq_huff.h.
+hipError_t launch_read_strings(const DevTables &t, const uint8_t *blk, uint64_t blk_len, const uint64_t *pos,
+                               const uint64_t *limit, const uint8_t *prefix, uint64_t n, uint8_t *out,
+                               uint64_t out_cap, uint64_t *out_off, uint32_t *out_len, uint8_t *status,
+                               uint64_t *next, hipStream_t s);
+hipError_t launch_write_strings(const DevTables &t, const uint8_t *in, const uint64_t *in_off, uint64_t n,
+                                const uint8_t *prefix, const uint8_t *lead, uint32_t choice, uint8_t *out,
+                                uint64_t out_cap, uint64_t *out_off, uint8_t *status, hipStream_t s);
 hipError_t launch_capacity(const uint64_t *in_off, uint64_t n, uint64_t base, uint64_t *cap_off,
                            hipStream_t s);
 

@@ -336,4 +336,117 @@ int mhq_huff_decode_dev(mhq_ctx *ctx, int dev, const uint8_t *in, const uint64_t
                                    (hipStream_t)stream));
 }
 
+int mhq_read_strings_dev(mhq_ctx *ctx, int dev, const uint8_t *blk, uint64_t blk_len, const uint64_t *pos,
+                         const uint64_t *limit, const uint8_t *prefix, uint64_t n, uint8_t *out, uint64_t out_cap,
+                         uint64_t *out_off, uint32_t *out_len, uint8_t *status, uint64_t *next, void *stream) {
+  Device *d = device(ctx, dev);
+  if (!d || !out_off || (n && (!blk || !pos || !limit || !prefix || !out || !out_len || !status || !next)))
+    return MHQ_EINVAL;
+  if (out_cap < blk_len / 5 * 8 + (blk_len % 5) * 8 / 5 + 1) return MHQ_EINVAL;
+  MHQ_TRY(hipSetDevice(d->ordinal));
+  return hip_rc(mhq::launch_read_strings(d->tables, blk, blk_len, pos, limit, prefix, n, out, out_cap, out_off,
+                                         out_len, status, next, (hipStream_t)stream));
+}
+
+int mhq_write_strings_dev(mhq_ctx *ctx, int dev, const uint8_t *in, const uint64_t *in_off, uint64_t n,
+                          const uint8_t *prefix, const uint8_t *lead, int choice, uint8_t *out, uint64_t out_cap,
+                          uint64_t *out_off, uint8_t *status, void *stream) {
+  Device *d = device(ctx, dev);
+  if (!d || !out_off || choice < MHQ_HUFF_AUTO || choice > MHQ_HUFF_NEVER) return MHQ_EINVAL;
+  if (n && (!in_off || !prefix || !lead || (out && !status))) return MHQ_EINVAL;
+  MHQ_TRY(hipSetDevice(d->ordinal));
+  return hip_rc(mhq::launch_write_strings(d->tables, in, in_off, n, prefix, lead, (uint32_t)choice, out, out_cap,
+                                          out_off, status, (hipStream_t)stream));
+}
+
+}  // extern "C"
+
+namespace {
+
+template <class T>
+struct DevArray {  // one call's device copy of a host array
+  T *p = nullptr;
+  ~DevArray() {
+    if (p) (void)hipFree(p);
+  }
+  hipError_t alloc(uint64_t count) { return hipMalloc((void **)&p, (count ? count : 1) * sizeof(T)); }
+  hipError_t put(const T *src, uint64_t count, hipStream_t s) {
+    hipError_t e = alloc(count);
+    if (e == hipSuccess && count) e = hipMemcpyAsync(p, src, count * sizeof(T), hipMemcpyHostToDevice, s);
+    return e;
+  }
+  hipError_t get(T *dst, uint64_t count, hipStream_t s) const {
+    return count ? hipMemcpyAsync(dst, p, count * sizeof(T), hipMemcpyDeviceToHost, s) : hipSuccess;
+  }
+};
+
+}  // namespace
+
+extern "C" {
+
+int mhq_read_strings(mhq_ctx *ctx, const uint8_t *blk, uint64_t blk_len, const uint64_t *pos, const uint64_t *limit,
+                     const uint8_t *prefix, uint64_t n, uint8_t *out, uint64_t out_cap, uint64_t *out_off,
+                     uint32_t *out_len, uint8_t *status, uint64_t *next) {
+  Device *d = device(ctx, 0);
+  if (!d || !out_off || (n && (!blk || !pos || !limit || !prefix || !out || !out_len || !status || !next)))
+    return MHQ_EINVAL;
+  if (out_cap < blk_len / 5 * 8 + (blk_len % 5) * 8 / 5 + 1) return MHQ_EINVAL;
+  std::lock_guard<std::mutex> lock(d->mu);
+  MHQ_TRY(hipSetDevice(d->ordinal));
+  hipStream_t s = d->stream;
+  DevArray<uint8_t> dblk, dprefix, dout, dst;
+  DevArray<uint64_t> dpos, dlim, doff, dnext;
+  DevArray<uint32_t> dlen;
+  MHQ_TRY(dblk.put(blk, blk_len, s));
+  MHQ_TRY(dpos.put(pos, n, s));
+  MHQ_TRY(dlim.put(limit, n, s));
+  MHQ_TRY(dprefix.put(prefix, n, s));
+  MHQ_TRY(dout.alloc(out_cap));
+  MHQ_TRY(doff.alloc(n + 1));
+  MHQ_TRY(dlen.alloc(n));
+  MHQ_TRY(dst.alloc(n));
+  MHQ_TRY(dnext.alloc(n));
+  MHQ_TRY(mhq::launch_read_strings(d->tables, dblk.p, blk_len, dpos.p, dlim.p, dprefix.p, n, dout.p, out_cap,
+                                   doff.p, dlen.p, dst.p, dnext.p, s));
+  MHQ_TRY(doff.get(out_off, n + 1, s));
+  MHQ_TRY(hipStreamSynchronize(s));
+  MHQ_TRY(dout.get(out, std::min<uint64_t>(out_off[n], out_cap), s));
+  MHQ_TRY(dlen.get(out_len, n, s));
+  MHQ_TRY(dst.get(status, n, s));
+  MHQ_TRY(dnext.get(next, n, s));
+  return hip_rc(hipStreamSynchronize(s));
+}
+
+int mhq_write_strings(mhq_ctx *ctx, const uint8_t *in, const uint64_t *in_off, uint64_t n, const uint8_t *prefix,
+                      const uint8_t *lead, int choice, uint8_t *out, uint64_t out_cap, uint64_t *out_off,
+                      uint8_t *status) {
+  Device *d = device(ctx, 0);
+  if (!d || !out_off || choice < MHQ_HUFF_AUTO || choice > MHQ_HUFF_NEVER) return MHQ_EINVAL;
+  if (n && (!in_off || !prefix || !lead || (out && !status))) return MHQ_EINVAL;
+  std::lock_guard<std::mutex> lock(d->mu);
+  MHQ_TRY(hipSetDevice(d->ordinal));
+  hipStream_t s = d->stream;
+  const uint64_t base = n ? in_off[0] : 0, bytes = n ? in_off[n] - in_off[0] : 0;
+  std::vector<uint64_t> rel(n + 1);
+  for (uint64_t i = 0; i <= n; i++) rel[i] = n ? in_off[i] - base : 0;
+  DevArray<uint8_t> din, dprefix, dlead, dout, dst;
+  DevArray<uint64_t> doff, dout_off;
+  MHQ_TRY(din.put(in, bytes, s));
+  MHQ_TRY(doff.put(rel.data(), n + 1, s));
+  MHQ_TRY(dprefix.put(prefix, n, s));
+  MHQ_TRY(dlead.put(lead, n, s));
+  MHQ_TRY(dout_off.alloc(n + 1));
+  MHQ_TRY(dst.alloc(n));
+  if (out) MHQ_TRY(dout.alloc(out_cap));
+  MHQ_TRY(mhq::launch_write_strings(d->tables, din.p, doff.p, n, dprefix.p, dlead.p, (uint32_t)choice,
+                                    out ? dout.p : nullptr, out_cap, dout_off.p, dst.p, s));
+  MHQ_TRY(dout_off.get(out_off, n + 1, s));
+  MHQ_TRY(hipStreamSynchronize(s));
+  if (out) {
+    MHQ_TRY(dout.get(out, std::min<uint64_t>(out_off[n], out_cap), s));
+    MHQ_TRY(dst.get(status, n, s));
+  }
+  return hip_rc(hipStreamSynchronize(s));
+}
+
 }  // extern "C"

@@ -162,6 +162,52 @@ class Codec:
                                       _p(status, C.c_uint8)), "mhq_huff_decode")
         return out, cap_off, out_len[:n], status[:n]
 
+    # ---------------- string literals (hc/io.go:73-97, 153-197) ---------------
+    def read_strings(self, blk: bytes, pos: Sequence[int], prefix: Sequence[int],
+                     limit: Optional[Sequence[int]] = None):
+        """Batch Reader.ReadString: literal i at byte pos[i] (H bit = bit 7-prefix[i])
+        reading up to limit[i] (default: the end of blk).  Returns
+        (values, status, next) with status MHQ_STR_* per literal."""
+        n = len(pos)
+        blk_a = _nonempty(np.frombuffer(bytes(blk), dtype=np.uint8).copy())
+        pos_a = _nonempty(np.ascontiguousarray(pos, dtype=np.uint64))
+        lim_a = _nonempty(np.ascontiguousarray(limit if limit is not None else [len(blk)] * n, dtype=np.uint64))
+        pf_a = _nonempty(np.ascontiguousarray(prefix, dtype=np.uint8))
+        cap = len(blk) * 8 // 5 + 16
+        out = np.zeros(cap, dtype=np.uint8)
+        out_off = np.zeros(n + 1, dtype=np.uint64)
+        out_len = np.zeros(max(n, 1), dtype=np.uint32)
+        status = np.zeros(max(n, 1), dtype=np.uint8)
+        nxt = np.zeros(max(n, 1), dtype=np.uint64)
+        check(self._L.mhq_read_strings(self._h, _p(blk_a, C.c_uint8), len(blk), _p(pos_a, C.c_uint64),
+                                       _p(lim_a, C.c_uint64), _p(pf_a, C.c_uint8), n, _p(out, C.c_uint8), cap,
+                                       _p(out_off, C.c_uint64), _p(out_len, C.c_uint32), _p(status, C.c_uint8),
+                                       _p(nxt, C.c_uint64)), "mhq_read_strings")
+        vals = [out[int(out_off[i]): int(out_off[i]) + int(out_len[i])].tobytes() for i in range(n)]
+        return vals, status[:n].copy(), nxt[:n].copy()
+
+    def write_strings(self, strs: Sequence[bytes], prefix: Sequence[int], lead: Optional[Sequence[int]] = None,
+                      choice: int = HuffmanCodingAuto) -> List[bytes]:
+        """Batch Writer.WriteStringRaw(s, prefix, choice) after opcode bits lead[i]."""
+        n = len(strs)
+        data, off = pack(strs)
+        data = _nonempty(data)
+        pf_a = _nonempty(np.ascontiguousarray(prefix, dtype=np.uint8))
+        ld_a = _nonempty(np.ascontiguousarray(lead if lead is not None else [0] * n, dtype=np.uint8))
+        out_off = np.zeros(n + 1, dtype=np.uint64)
+        check(self._L.mhq_write_strings(self._h, _p(data, C.c_uint8), _p(off, C.c_uint64), n, _p(pf_a, C.c_uint8),
+                                        _p(ld_a, C.c_uint8), choice, None, 0, _p(out_off, C.c_uint64), None),
+              "mhq_write_strings (size)")
+        cap = int(out_off[-1]) if n else 0
+        out = np.zeros(max(cap, 1), dtype=np.uint8)
+        status = np.zeros(max(n, 1), dtype=np.uint8)
+        check(self._L.mhq_write_strings(self._h, _p(data, C.c_uint8), _p(off, C.c_uint64), n, _p(pf_a, C.c_uint8),
+                                        _p(ld_a, C.c_uint8), choice, _p(out, C.c_uint8), cap,
+                                        _p(out_off, C.c_uint64), _p(status, C.c_uint8)), "mhq_write_strings")
+        if n and np.any(status[:n] != _lib.MHQ_STR_OK):
+            raise RuntimeError("mhq_write_strings: output buffer too small")
+        return unpack(out, out_off)
+
     # ---------------- device-resident batches (torch tensors on one device) ---
     @staticmethod
     def _stream(stream):
@@ -238,6 +284,32 @@ def HuffmanDecodeBatch(enc: Sequence[bytes], codec: Optional[Codec] = None
     vals = unpack(out, cap_off, out_len)
     errs = [InvalidHuffmanCoding() if s == _lib.MHQ_LIT_INVALID else None for s in status]
     return vals, errs
+
+
+class StringEOF(EOFError):
+    """io.EOF from Reader.ReadString (hc/io.go:92-94)."""
+
+
+def ReadStringBatch(blk: bytes, pos: Sequence[int], prefix: Sequence[int], limit: Optional[Sequence[int]] = None,
+                    codec: Optional[Codec] = None) -> Tuple[List[bytes], List[Optional[Exception]], List[int]]:
+    """Per literal: Reader.ReadString(prefix[i]) at pos[i] (hc/io.go:73-97);
+    returns (values, errors, next positions)."""
+    codec = codec or default_codec()
+    vals, status, nxt = codec.read_strings(blk, pos, prefix, limit)
+    errs: List[Optional[Exception]] = []
+    for st in status:
+        errs.append(InvalidHuffmanCoding() if st == _lib.MHQ_STR_INVALID
+                    else StringEOF() if st == _lib.MHQ_STR_EOF
+                    else RuntimeError("output buffer too small") if st == _lib.MHQ_STR_NOSPACE else None)
+    return vals, errs, [int(x) for x in nxt]
+
+
+def WriteStringRawBatch(strs: Sequence[bytes], prefix: Sequence[int], choice: int = HuffmanCodingAuto,
+                        lead: Optional[Sequence[int]] = None, codec: Optional[Codec] = None) -> List[bytes]:
+    """Per string: Writer.WriteStringRaw(s, prefix[i], choice) (hc/io.go:153-197),
+    the frame starting with opcode bits lead[i] above the H bit."""
+    codec = codec or default_codec()
+    return codec.write_strings(strs, prefix, lead, choice)
 
 
 def HuffmanChoose(raw_len: int, enc_len: int, choice: int = HuffmanCodingAuto) -> bool:

@@ -1,0 +1,140 @@
+"""String-literal framing on the GPU: batch Reader.ReadString / Writer.WriteStringRaw
+(hc/io.go:73-97, 153-197, with the prefix integers of hc/io.go:25-55, 110-137)
+through the C ABI, bit-exact against the CPU oracle (oracle/huff_oracle.c
+orc_read_string / orc_write_string) and the reference's own vectors
+(hc/io_test.go:77-88, tests/golden/string_vectors.json).
+"""
+import random
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+OK, INVALID, EOF = 0, 1, 2
+ORC_EOF, ORC_INVALID = -1, 1
+
+
+@pytest.fixture(scope="module")
+def codec():
+    from minhq_amd import build, hc
+
+    build.build()
+    c = hc.Codec(1)
+    yield c
+    c.close()
+
+
+def _oracle_status(rc):
+    return {0: OK, ORC_INVALID: INVALID, ORC_EOF: EOF}[rc]
+
+
+def test_reference_vectors_read(codec, golden):  # hc/io_test.go:90-101
+    vecs = golden("string_vectors.json")
+    blk, pos = b"", []
+    for v in vecs:  # every literal in a block of its own: limits at its end
+        pos.append(len(blk))
+        blk += bytes.fromhex(v["hex"])
+    limits = pos[1:] + [len(blk)]
+    vals, st, nxt = codec.read_strings(blk, pos, [v["prefix"] for v in vecs], limits)
+    for v, val, s, e, lim in zip(vecs, vals, st, nxt, limits):
+        assert (val, s) == (v["text"].encode(), OK), v["src"]
+        assert e == lim
+
+
+def test_reference_vectors_write(codec, golden):  # hc/io_test.go:103-118: Auto picks the shorter form
+    from minhq_amd import hc
+
+    vecs = golden("string_vectors.json")
+    raw, huf = {}, {}
+    for v in vecs:
+        b = bytes.fromhex(v["hex"])
+        (huf if b[0] & 0x80 else raw)[v["text"]] = b
+    # Auto sends the Huffman form only when it is strictly shorter (hc/io.go:172)
+    by_text = {t: huf[t] if len(huf[t]) < len(raw[t]) else raw[t] for t in raw}
+    texts = sorted(by_text)
+    frames = hc.WriteStringRawBatch([t.encode() for t in texts], [7] * len(texts), codec=codec)
+    assert frames == [by_text[t] for t in texts]
+
+
+def _random_strings(rng, n):
+    alpha = b"abcdefghijklmnopqrstuvwxyz0123456789-_./:;=, "
+    out = []
+    for _ in range(n):
+        kind = rng.random()
+        L = rng.choice([0, 1, 2, 5, 30, 126, 127, 128, 200, 300]) if kind < 0.3 else rng.randint(0, 60)
+        if rng.random() < 0.8:
+            out.append(bytes(rng.choice(alpha) for _ in range(L)))
+        else:
+            out.append(bytes(rng.randrange(256) for _ in range(L)))
+    return out
+
+
+@pytest.mark.parametrize("choice", [0, 1, 2])
+def test_write_matches_oracle(codec, oracle_mod, choice):
+    rng = random.Random(7 + choice)
+    strs = _random_strings(rng, 1500)
+    prefixes = [rng.choice([7, 5, 3]) for _ in strs]
+    leads = [rng.randrange(1 << (7 - p)) if p < 7 else 0 for p in prefixes]
+    frames = codec.write_strings(strs, prefixes, leads, choice)
+    for s, p, ld, f in zip(strs, prefixes, leads, frames):
+        assert f == oracle_mod.write_string(s, prefix=p, choice=choice, lead=ld, lead_bits=7 - p)
+
+
+def test_read_matches_oracle(codec, oracle_mod):
+    """A block of framed literals (every choice, prefixes 7/5/3, opcode bits
+    above): each read from its start to the block end, as the oracle does."""
+    rng = random.Random(11)
+    strs = _random_strings(rng, 1500)
+    blk, pos, prefixes = b"", [], []
+    for s in strs:
+        p = rng.choice([7, 5, 3])
+        ld = rng.randrange(1 << (7 - p)) if p < 7 else 0
+        pos.append(len(blk))
+        prefixes.append(p)
+        blk += oracle_mod.write_string(s, prefix=p, choice=rng.choice([0, 1, 2]), lead=ld, lead_bits=7 - p)
+    vals, st, nxt = codec.read_strings(blk, pos, prefixes)
+    for i, (s, p) in enumerate(zip(strs, prefixes)):
+        ref, rc, used = oracle_mod.read_string(blk[pos[i]:], prefix=p, skip_bits=7 - p)
+        assert (vals[i], int(st[i])) == (ref, _oracle_status(rc)), i
+        assert vals[i] == s or rc != 0
+        assert int(nxt[i]) == pos[i] + used
+
+
+def test_read_edge_cases(codec, oracle_mod):
+    """Truncated blocks, empty literals, invalid codes, header EOF and integer
+    overflow -- each checked against the oracle's ReadString restatement."""
+    cases = [
+        bytes.fromhex("80"),                      # Huffman, length 0: io.EOF
+        bytes.fromhex("00"),                      # raw, length 0: ("", nil)
+        bytes.fromhex("81ff"),                    # Huffman padding only: io.EOF
+        bytes.fromhex("84ffffffff"),              # EOS prefix + a 31st bit: invalid
+        bytes.fromhex("843fffffff"),              # "o" then a partial code: ok
+        bytes.fromhex("8bc65a283fd29c"),          # Huffman "Hello, World!" cut by the block end
+        bytes.fromhex("0d48656c6c"),              # raw cut by the block end
+        bytes.fromhex("05"),                      # raw, payload entirely missing: io.EOF
+        bytes.fromhex("7f"),                      # length continuation missing: ("", nil)
+        bytes.fromhex("7f8080808080808080808002"),  # ReadInt overflow: ("", nil)
+        bytes.fromhex("7f00") + b"x" * 127,       # 127-byte raw literal (one continuation octet)
+        b"",                                      # nothing to read: ("", nil)
+    ]
+    for c in cases:
+        vals, st, nxt = codec.read_strings(c, [0], [7], [len(c)])
+        ref, rc, used = oracle_mod.read_string(c, prefix=7)
+        assert (vals[0], int(st[0]), int(nxt[0])) == (ref, _oracle_status(rc), used), c.hex()
+
+
+def test_read_all_prefixes(codec, oracle_mod):
+    rng = random.Random(5)
+    for p in range(1, 8):
+        strs = _random_strings(rng, 200)
+        blk, pos = b"", []
+        for s in strs:
+            pos.append(len(blk))
+            blk += oracle_mod.write_string(s, prefix=p, choice=rng.choice([0, 1, 2]),
+                                           lead=rng.randrange(1 << (7 - p)) if p < 7 else 0, lead_bits=7 - p)
+        vals, st, _ = codec.read_strings(blk, pos, [p] * len(strs))
+        for i, s in enumerate(strs):
+            ref, rc, _ = oracle_mod.read_string(blk[pos[i]:], prefix=p, skip_bits=7 - p)
+            assert (vals[i], int(st[i])) == (ref, _oracle_status(rc))
+            # every literal reads back, except an empty one sent Huffman-coded: io.EOF (hc/io.go:92-94)
+            assert vals[i] == s and (int(st[i]) == OK or (s == b"" and int(st[i]) == EOF))

@@ -46,10 +46,21 @@ def timeline_report(fn):
     buf = (ctypes.c_ulonglong * (W * S))()
     fn(buf, W * S)
     a = np.frombuffer(buf, dtype=np.uint64).reshape(W, S).astype(np.int64)
+    wave_id = np.nonzero(a[:, 0] > 0)[0]
     a = a[a[:, 0] > 0]
     t0 = a[:, 0].min()
     us = lambda x: (x - t0) / 100.0  # 100 MHz ticks -> us
     end = us(a[:, S - 1])
+    blk = wave_id // 16
+    blk_end = {}
+    for b_, e_ in zip(blk, end):
+        blk_end[b_] = max(blk_end.get(b_, 0.0), e_)
+    be = np.array([blk_end[b_] for b_ in sorted(blk_end)])
+    bx = np.array(sorted(blk_end)) % 8
+    print("  workgroup end by XCD (blockIdx % 8): " + " ".join(
+        f"{x}:{be[bx == x].mean():.1f}/{be[bx == x].max():.1f}" for x in range(8)) +
+        f"  | workgroup end p10 {np.percentile(be, 10):.1f} p50 {np.percentile(be, 50):.1f} max {be.max():.1f}",
+        file=sys.stderr)
     print(f"timeline: {a.shape[0]} waves, start spread {us(a[:, 0]).max():.2f} us, end max {end.max():.2f} "
           f"p50 {np.percentile(end, 50):.2f} p10 {np.percentile(end, 10):.2f} us", file=sys.stderr)
     prev = a[:, 0]
