@@ -24,6 +24,8 @@
 //     thread straight from global memory.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "huff_common.h"
 #include "huff_kernels.h"
 #include "huff_table.h"
@@ -304,14 +306,88 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu((kT / 64 * M
   if (kEmit && pending) store_out(pd_o, (const uint8_t *)sm.out_w, pd_lo, pd_hi, tid, kT);
 }
 
+// ---- encode_len: sum of code lengths per literal --------------------------
+// One thread per literal, reading its bytes as aligned 16-B chunks straight
+// from global memory, the first kPre of them in one go (one memory round trip
+// for a literal of up to 64 bytes; neighbouring lanes read neighbouring
+// literals, so a wave's loads cover one contiguous stretch); no staging, no
+// sort.  (A grid-stride variant with the next literal's loads in flight ran
+// slower: fewer waves hide less.)  The code lengths sit in LDS one per dword,
+// so lanes that look up different bytes rarely share a bank.  Per byte: the shifted
+// byte as address, one LDS read, the chunk's in-range mask bit times the
+// length added in.
+constexpr int kLenT = 256;
+constexpr int kPre = 5;  // chunks loaded ahead: literals of up to 64 bytes
+
+struct LenAhead {
+  uint64_t a, b;   // byte range (bias removed)
+  u32x4 v[kPre];   // its first kPre chunks
+};
+
+__device__ __forceinline__ void len_load_chunks(LenAhead &t, const uint8_t *__restrict__ in) {
+  const uint64_t c0 = t.a & ~(uint64_t)15;
+  const u32x4 *src = (const u32x4 *)(in + c0);  // aligned chunks holding a valid byte: in bounds
+  const uint64_t nchunks = t.b > t.a ? (t.b - c0 + 15) / 16 : 0;
+#pragma unroll
+  for (int j = 0; j < kPre; j++)
+    if ((uint64_t)j < nchunks) t.v[j] = __builtin_nontemporal_load(src + j);
+}
+
+__device__ __forceinline__ uint32_t len_sum(const LenAhead &t, const uint8_t *__restrict__ in,
+                                            const uint32_t *lens) {
+  const uint64_t a = t.a, b = t.b;
+  uint32_t bits = 0;
+  const uint64_t c0 = a & ~(uint64_t)15;
+  const uint64_t nchunks = b > a ? (b - c0 + 15) / 16 : 0;
+  auto add_chunk = [&](const u32x4 &x, uint64_t c) {
+    const uint32_t w[4] = {x.x, x.y, x.z, x.w};
+    // bytes of this chunk inside [a, b): bits [lo, hi) of m
+    const uint32_t lo = c < a ? (uint32_t)(a - c) : 0u, hi = b - c < 16 ? (uint32_t)(b - c) : 16u;
+    const uint32_t m = ((1u << hi) - 1u) & ~((1u << lo) - 1u);
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+      const uint32_t l = lens[(w[k >> 2] >> (8 * (k & 3))) & 0xffu];
+      bits = __builtin_amdgcn_ubfe(m, k, 1) * l + bits;
+    }
+  };
+#pragma unroll
+  for (int j = 0; j < kPre; j++)
+    if ((uint64_t)j < nchunks) add_chunk(t.v[j], c0 + 16u * j);
+  if (nchunks > (uint64_t)kPre) {  // a long literal: the rest one chunk ahead
+    const u32x4 *src = (const u32x4 *)(in + c0);
+    u32x4 nx = __builtin_nontemporal_load(src + kPre);
+    for (uint64_t j = kPre; j < nchunks; j++) {
+      const u32x4 cur = nx;
+      if (j + 1 < nchunks) nx = __builtin_nontemporal_load(src + j + 1);
+      add_chunk(cur, c0 + 16u * j);
+    }
+  }
+  return bits;
+}
+
+__global__ __launch_bounds__(kLenT) void encode_len_kernel(const uint8_t *__restrict__ in,
+                                                           const uint64_t *__restrict__ in_off, uint64_t in_bias,
+                                                           uint64_t n, uint32_t *__restrict__ enc_len,
+                                                           const uint8_t *__restrict__ g_len) {
+  __shared__ uint32_t lens[256];
+  lens[threadIdx.x] = g_len[threadIdx.x];
+  __syncthreads();
+  const uint64_t i = (uint64_t)blockIdx.x * kLenT + threadIdx.x;
+  if (i >= n) return;
+  LenAhead t{};
+  t.a = in_off[i] - in_bias;
+  t.b = in_off[i + 1] - in_bias;
+  len_load_chunks(t, in);
+  enc_len[i] = (len_sum(t, in, lens) + 7u) >> 3;
+}
+
 }  // namespace
 
 hipError_t launch_encode_len(const DevTables &t, const uint8_t *in, const uint64_t *in_off, uint64_t in_bias,
                              uint64_t n, uint32_t *enc_len, hipStream_t s) {
   if (n == 0) return hipSuccess;
-  const unsigned grid = dev::tile_grid((n + kT - 1) / kT, 1, MHQ_ENC_BLOCKS * MHQ_PER_CU);
-  encode_kernel<false><<<dim3(grid), dim3(kT), 0, s>>>(in, in_off, in_bias, n, nullptr, nullptr, 0, enc_len, t.code,
-                                                        t.len, (n + grid - 1) / grid);
+  encode_len_kernel<<<dim3((unsigned)((n + kLenT - 1) / kLenT)), dim3(kLenT), 0, s>>>(in, in_off, in_bias, n,
+                                                                                      enc_len, t.len);
   return hipGetLastError();
 }
 
