@@ -134,22 +134,20 @@ __device__ __forceinline__ void zero_lds(uint32_t *lds, uint32_t nbytes, int lan
 }
 
 // Writes LDS bytes [lo, hi) to global o_al + [lo, hi), o_al 16-B aligned.
-// Whole 16-B chunks go out as one aligned store; the (at most two) partial
-// chunks at the ends are written byte by byte so neighbours are untouched.
-// `lane` / `nthreads`: this thread's index among the threads sharing the copy.
+// Whole 16-B chunks go out as one aligned store each; the bytes of the (at
+// most two) partial chunks at the ends, at most 15 each, are written one per
+// thread by threads 0-15 (head) and 16-31 (tail), all in one pass, so
+// neighbours are untouched.  `lane` / `nthreads` (>= 32): this thread's index
+// among the threads sharing the copy.
 __device__ __forceinline__ void store_out(uint8_t *o_al, const uint8_t *lds, uint32_t lo, uint32_t hi, int lane,
                                           uint32_t nthreads = kWave) {
   if (hi <= lo) return;
-  const uint32_t c0 = lo >> 4, c1 = (hi + 15u) >> 4;
-  for (uint32_t c = c0 + lane; c < c1; c += nthreads) {
-    const uint32_t a = c << 4, b = a + 16u;
-    if (a >= lo && b <= hi) {
-      __builtin_nontemporal_store(*(const u32x4 *)(lds + a), (u32x4 *)(o_al + a));
-    } else {
-      const uint32_t x0 = a > lo ? a : lo, x1 = b < hi ? b : hi;
-      for (uint32_t x = x0; x < x1; x++) o_al[x] = lds[x];
-    }
-  }
+  const uint32_t f0 = (lo + 15u) >> 4, f1 = hi >> 4;  // whole chunks [f0, f1)
+  for (uint32_t c = f0 + lane; c < f1; c += nthreads)
+    __builtin_nontemporal_store(*(const u32x4 *)(lds + (c << 4)), (u32x4 *)(o_al + (c << 4)));
+  const uint32_t head_end = min(hi, f0 << 4), tail_start = max(head_end, f1 << 4);
+  const uint32_t x = lane < 16 ? lo + (uint32_t)lane : tail_start + (uint32_t)lane - 16u;
+  if (lane < 32 && x < (lane < 16 ? head_end : hi)) o_al[x] = lds[x];
 }
 
 __device__ __forceinline__ uint32_t lds_byte(const uint32_t *w, uint32_t x) {

@@ -30,6 +30,7 @@
 using namespace mhq;
 
 constexpr int kStreamBytes = 32768;
+constexpr uint32_t kLut1Null = 0u;  // (variants 0-4 predate the byte-field LUT1 layout; time 5-8 only)
 constexpr int kStreamWords = kStreamBytes / 4;
 
 struct Smem {
@@ -183,7 +184,7 @@ __device__ uint32_t run(const Smem &sm, uint32_t *out_w, uint32_t p0, uint32_t p
       b.refill();
     }
     chk += a.p + b.p;
-  } else if constexpr (V == 5 || V == 6 || V == 7) {
+  } else if constexpr (V == 5 || V == 6 || V == 7 || V == 9 || V == 10) {
     // lean loop: SDWA-friendly entries (byte0 tot, byte1 nsym, byte2 sym0, byte3 sym1; 0 = long),
     // one long check per 2 probes; V5 writes symbols with ds_write_b16 (unaligned), V6 with two
     // ds_write_b8, V7 through the 64-bit accumulator + ds_or.
@@ -220,16 +221,68 @@ __device__ uint32_t run(const Smem &sm, uint32_t *out_w, uint32_t p0, uint32_t p
           out.put(e >> 16, (e >> 8) & 0xffu);
         }
       }
+      if constexpr (V == 10) {  // timing bound: no flush store, the accumulator drains in registers
+        chk ^= (uint32_t)out.acc;
+        out.acc >>= out.ab & 32u;
+        out.ab &= 31u;
+      }
       {
         const bool need = nb <= 32u;
         in.bb |= (uint64_t)(need ? in.w : 0u) << ((32u - nb) & 63u);
         in.kb += need ? 32u : 0u;
         nb += need ? 32u : 0u;
-        in.w = in.in_w[in.kb >> 5];
+        if constexpr (V == 9) {
+          in.w = in.kb * 0x9e3779b9u;  // timing bound: no refill read (wrong bits)
+        } else {
+          in.w = in.in_w[in.kb >> 5];
+        }
       }
-      if constexpr (V == 7) out.flush(out_w);
+      if constexpr (V == 7 || V == 9) out.flush(out_w);
     }
     chk += nb + optr + out.ow;
+  } else if constexpr (V == 8) {
+    // two independent lean chains per lane (acc + ds_or), interleaved probe by probe
+    const uint32_t *lutL = sm.lutL;
+    BitBuf in[2];
+    uint32_t nb[2];
+    OutAcc out[2];
+    const uint32_t ps[2] = {p0, p1};
+#pragma unroll
+    for (int c = 0; c < 2; c++) {
+      in[c].init(sm.in_w, ps[c]);
+      nb[c] = 64u - (ps[c] & 31u);
+      out[c].init(lane * 128u + c * 64u + (ps[c] & 3u));
+    }
+    for (uint32_t i = 0; i < probes; i += 2) {
+#pragma unroll
+      for (int u = 0; u < 2; u++) {
+#pragma unroll
+        for (int c = 0; c < 2; c++) {
+          uint32_t e = lutL[in[c].top32() >> (32 - kLut1Bits)];
+          if (u == 1 && e == 0) {
+            in[c].p = in[c].kb - nb[c];
+            in[c].refill();
+            nb[c] = in[c].kb - in[c].p;
+            uint32_t sym = 0;
+            const uint32_t L = long_code(sm.lut2, in[c].top32(), sym);
+            e = L | (8u << 8) | (sym << 16);
+          }
+          in[c].bb <<= (e & 63u);
+          nb[c] -= e & 0xffu;
+          out[c].put(e >> 16, (e >> 8) & 0xffu);
+        }
+      }
+#pragma unroll
+      for (int c = 0; c < 2; c++) {
+        const bool need = nb[c] <= 32u;
+        in[c].bb |= (uint64_t)(need ? in[c].w : 0u) << ((32u - nb[c]) & 63u);
+        in[c].kb += need ? 32u : 0u;
+        nb[c] += need ? 32u : 0u;
+        in[c].w = in[c].in_w[in[c].kb >> 5];
+        out[c].flush(out_w);
+      }
+    }
+    chk += nb[0] + nb[1] + out[0].ow + out[1].ow;
   } else {
     uint32_t p = p0;
     for (uint32_t i = 0; i < probes; i++) {
@@ -345,7 +398,7 @@ int main(int argc, char **argv) {
   CHECK(hipEventCreate(&e0));
   CHECK(hipEventCreate(&e1));
   const char *names[] = {"regbuf+ds_or", "regbuf,no-out", "regbuf+ds_or,1chk", "regbuf,2chains,no-out", "window,no-out",
-                         "lean,ds_write_b16", "lean,2x ds_write_b8", "lean,acc+ds_or"};
+                         "lean,ds_write_b16", "lean,2x ds_write_b8", "lean,acc+ds_or", "lean,acc+ds_or,2chains", "lean,no refill read", "lean,no flush"};
   // host decode for the correctness check: (len, code) -> symbol
   auto host_decode = [&](uint64_t p, int nsym, std::vector<uint8_t> &outv) {
     outv.clear();
@@ -374,6 +427,9 @@ int main(int argc, char **argv) {
       case 5: ubench<5><<<grid, block>>>(d_lutL, d_lut1, d_lut2, d_words, d_starts, starts.size(), probes, d_sink, d_cyc); break;
       case 6: ubench<6><<<grid, block>>>(d_lutL, d_lut1, d_lut2, d_words, d_starts, starts.size(), probes, d_sink, d_cyc); break;
       case 7: ubench<7><<<grid, block>>>(d_lutL, d_lut1, d_lut2, d_words, d_starts, starts.size(), probes, d_sink, d_cyc); break;
+      case 8: ubench<8><<<grid, block>>>(d_lutL, d_lut1, d_lut2, d_words, d_starts, starts.size(), probes, d_sink, d_cyc); break;
+      case 9: ubench<9><<<grid, block>>>(d_lutL, d_lut1, d_lut2, d_words, d_starts, starts.size(), probes, d_sink, d_cyc); break;
+      case 10: ubench<10><<<grid, block>>>(d_lutL, d_lut1, d_lut2, d_words, d_starts, starts.size(), probes, d_sink, d_cyc); break;
     }
   };
   // correctness of the lean variants: one wave, 24 probes per lane, compare 40 output bytes
@@ -401,9 +457,9 @@ int main(int argc, char **argv) {
     printf("check %-22s: %s (%d byte mismatches in 64 lanes x 20 bytes)\n", names[v], bad ? "MISMATCH" : "ok", bad);
   }
   const int only_v = argc > 2 ? atoi(argv[2]) : -1, only_w = argc > 3 ? atoi(argv[3]) : 0;
-  for (int v = 5; v < 8; v++) {
+  for (int v = 7; v < 11; v++) {
     if (only_v >= 0 && v != only_v) continue;
-    for (int waves : {8, 12, 16}) {
+    for (int waves : {12, 16}) {
       if (only_w && waves != only_w) continue;
       launch(v, waves);
       CHECK(hipDeviceSynchronize());
@@ -417,7 +473,7 @@ int main(int argc, char **argv) {
       CHECK(hipEventElapsedTime(&ms, e0, e1));
       unsigned long long cyc = 0;
       CHECK(hipMemcpy(&cyc, d_cyc, 8, hipMemcpyDeviceToHost));
-      const double chains = (v == 3 ? 2.0 : 1.0);
+      const double chains = (v == 3 || v == 8 ? 2.0 : 1.0);
       const double lane_probes = (double)cus * waves * 64 * probes * chains * reps;
       const double wave_cyc = (double)cyc / ((double)cus * waves * reps);
       printf("%-24s waves/CU %2d: %7.3f ms  %8.1f Gprobe/s  wave-cycles/probe-step %6.1f  SIMD-cycles/wave-probe %5.1f\n",
