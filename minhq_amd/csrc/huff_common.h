@@ -24,6 +24,20 @@ __device__ __forceinline__ void wave_sync() {
 
 __device__ __forceinline__ uint32_t popc64(uint64_t m) { return (uint32_t)__popcll(m); }
 
+// Inclusive sum over lanes 0..lane of a full wave, in DPP moves (VALU only,
+// no LDS round trips): prefix sums inside rows of 16 by row_shr 1/2/4/8, then
+// row 15's total into rows 1 and 3 (row_bcast:15) and lane 31's into rows 2
+// and 3 (row_bcast:31).  Every lane must be active.
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, true);  // row_shr:1
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, true);  // row_shr:2
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, true);  // row_shr:4
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, true);  // row_shr:8
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);  // row_bcast:15
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);  // row_bcast:31
+  return x;
+}
+
 template <int kTileLits>
 struct TileOffsets {
   static constexpr int kPer = (kTileLits + 1 + kWave - 1) / kWave;

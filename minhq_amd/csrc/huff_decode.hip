@@ -464,14 +464,7 @@ __device__ __forceinline__ void decode_piece(const Smem &sm, WaveSmem &ws, uint3
   wave_sync();
   {
     const uint32_t hcount = ws.hist[lane];
-    uint32_t x = hcount;
-#pragma unroll
-    for (int d = 1; d < kWave; d <<= 1) {
-      const uint32_t y = __shfl_up(x, d);
-      if ((int)lane >= d) x += y;
-    }
-    wave_sync();
-    ws.hist[lane] = x - hcount;
+    ws.hist[lane] = wave_incl_scan(hcount) - hcount;
   }
   wave_sync();
 #pragma unroll
@@ -645,7 +638,7 @@ __global__ __launch_bounds__(kT) void decode_kernel(const uint8_t *__restrict__ 
   if (tid < 64) ((uint32_t *)sm.clen)[tid] = ((const uint32_t *)g_len)[tid];
   if (tid == 0) sm.next_tile = 3 * kWaves;
   TileIn tin;
-  load_in(tin, in, in_bias, uniform64(__shfl(off.i0, 0)), uniform64(off.ie), lane);
+  load_in(tin, in, in_bias, uniform64(off.i0), uniform64(off.ie), lane);
   __syncthreads();
   uint64_t pd_s = 0;  // the previous tile, still in the output slice: literals, output range
   uint32_t pd_m = 0, pd_lo = 0, pd_hi = 0;
@@ -655,7 +648,7 @@ __global__ __launch_bounds__(kT) void decode_kernel(const uint8_t *__restrict__ 
   while (tile < ntiles) {
     const uint64_t s = L0 + (uint64_t)tile * tl;
     const uint32_t cnt = (uint32_t)min((uint64_t)tl, L1 - s);
-    const uint64_t ib = uniform64(__shfl(off.i0, 0)), ob = uniform64(__shfl(off.o0, 0));
+    const uint64_t ib = uniform64(off.i0), ob = uniform64(off.o0);
     const uint64_t ie = uniform64(off.ie), oe = uniform64(off.oe);
     const uint8_t *ia = in + (ib - in_bias);
     uint8_t *oa = out + (ob - out_bias);
@@ -677,7 +670,7 @@ __global__ __launch_bounds__(kT) void decode_kernel(const uint8_t *__restrict__ 
       if (lane == 0) ws.rec[cnt] = (uint32_t)(ie - ib + idelta) | (uint32_t)(oe - ob + odelta) << 16;
     }
     // the next tile's input (its offsets arrived during the previous decode), the offsets of the one after
-    load_in(tin, in, in_bias, uniform64(__shfl(off2.i0, 0)), uniform64(off2.ie), lane);
+    load_in(tin, in, in_bias, uniform64(off2.i0), uniform64(off2.ie), lane);
     off = off2;
     load_off(off2, in_off, out_off, L0 + (uint64_t)tile3 * tl, L1, tl, lane);
     TL(1 + 3 * tl_j);

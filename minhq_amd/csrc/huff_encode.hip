@@ -274,13 +274,7 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu((kT / 64 * M
       __syncthreads();
       if (wave == 0) {
         const uint32_t h = sm.hist[lane];
-        uint32_t x = h;
-#pragma unroll
-        for (int d = 1; d < kWave; d <<= 1) {
-          const uint32_t y = __shfl_up(x, d);
-          if ((int)lane >= d) x += y;
-        }
-        sm.hist[lane] = x - h;
+        sm.hist[lane] = wave_incl_scan(h) - h;
       }
       __syncthreads();
       if (tid < m) sm.order[sm.hist[bk] + rk] = (uint16_t)tid;

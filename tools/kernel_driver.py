@@ -38,8 +38,8 @@ def batch_for(name: str, n: int):
 
 def timeline_report(fn):
     """Summarises the MHQ_DIAG_TIMELINE build's per-wave stamps (last launch):
-    slot 0 start, 63 end, tile j: 1+3j+k, k = 0 next loads issued, 1 previous
-    output flushed, 2 decoded."""
+    slot 0 start, 63 end, tile j: 1+5j+k, k = 0 next loads issued, 1 previous
+    output flushed, 2 sorted, 3 fast loop done, 4 decoded."""
     import ctypes
 
     W, S = 1024 * 16, 64
@@ -64,17 +64,19 @@ def timeline_report(fn):
     print(f"timeline: {a.shape[0]} waves, start spread {us(a[:, 0]).max():.2f} us, end max {end.max():.2f} "
           f"p50 {np.percentile(end, 50):.2f} p10 {np.percentile(end, 10):.2f} us", file=sys.stderr)
     prev = a[:, 0]
-    for j in range(20):
-        b = 1 + 3 * j
-        ok = a[:, b + 2] > 0
+    for j in range(12):
+        b = 1 + 5 * j
+        ok = a[:, b + 4] > 0
         if not ok.any():
             break
         x = a[ok]
         pv = prev[ok]
-        print(f"  tile {j}: waves={ok.sum()} stage {(x[:, b] - pv).mean() / 100:.2f} flush {(x[:, b + 1] - x[:, b]).mean() / 100:.2f} "
-              f"decode {(x[:, b + 2] - x[:, b + 1]).mean() / 100:.2f} (p90 {np.percentile(x[:, b + 2] - x[:, b + 1], 90) / 100:.2f}) "
-              f"done@{us(x[:, b + 2]).mean():.2f}", file=sys.stderr)
-        prev = np.where(a[:, b + 2] > 0, a[:, b + 2], prev)
+        d = lambda k0, k1: (x[:, b + k1] - x[:, b + k0]).mean() / 100
+        print(f"  tile {j}: waves={ok.sum()} stage {(x[:, b] - pv).mean() / 100:.2f} flush {d(0, 1):.2f} "
+              f"sort {d(1, 2):.2f} fast {d(2, 3):.2f} tails {d(3, 4):.2f} "
+              f"(decode p90 {np.percentile(x[:, b + 4] - x[:, b + 1], 90) / 100:.2f}) "
+              f"done@{us(x[:, b + 4]).mean():.2f}", file=sys.stderr)
+        prev = np.where(a[:, b + 4] > 0, a[:, b + 4], prev)
 
 
 def main():
