@@ -159,6 +159,42 @@ int mhq_write_strings(mhq_ctx *ctx, const uint8_t *in, const uint64_t *in_off, u
                       const uint8_t *lead, int choice, uint8_t *out, uint64_t out_cap, uint64_t *out_off,
                       uint8_t *status);
 
+/* ---------------- prefix integers ------------------------------------------
+ * Batch Reader.ReadInt / ReadIndex(prefix) and Writer.WriteInt(v, prefix)
+ * (hc/io.go:25-67, 110-137), the integers of every HPACK/QPACK instruction
+ * (prefixes 3..8: hc/hpack.go:84-130, hc/qpackdecoder.go:145-393).  An integer
+ * starts on an octet whose low prefix bits hold its prefix; the bits above
+ * belong to the caller's opcode.  Sequential within a header block, the
+ * integers of many blocks (or the ones a host pre-pass has located) batch. */
+
+/* Per-integer outcome (status[]). */
+#define MHQ_INT_OK 0
+#define MHQ_INT_EOF 1      /* the block ended inside the integer (ReadBits: io.EOF) */
+#define MHQ_INT_OVERFLOW 2 /* ErrIntegerOverflow (hc/io.go:12,46; ReadIndex: hc/io.go:63) */
+#define MHQ_INT_BADARG 3   /* prefix outside 1..8 (not a reference outcome) */
+#define MHQ_INT_NOSPACE 4  /* write: the frame does not fit out_cap (not a reference outcome) */
+
+/* Reads n integers from blk: integer i starts at byte pos[i] and may use bytes
+ * up to limit[i].  Writes value[i], next[i] (the byte after the integer; pos[i]
+ * on error) and status[i].  index != 0 applies ReadIndex's check (value above
+ * the largest int64 -> MHQ_INT_OVERFLOW).  Device pointers; asynchronous on
+ * `stream`. */
+int mhq_read_ints_dev(mhq_ctx *ctx, int dev, const uint8_t *blk, const uint64_t *pos, const uint64_t *limit,
+                      const uint8_t *prefix, uint64_t n, int index, uint64_t *value, uint64_t *next,
+                      uint8_t *status, void *stream);
+/* Writes n integers as WriteInt(value[i], prefix[i]) after opcode bits lead[i]
+ * (the 8-prefix[i] bits above the prefix), back to back: integer i is
+ * out[out_off[i] .. out_off[i+1]).  out NULL: out_off only (size query).
+ * Device pointers; asynchronous on `stream`. */
+int mhq_write_ints_dev(mhq_ctx *ctx, int dev, const uint64_t *value, const uint8_t *prefix, const uint8_t *lead,
+                       uint64_t n, uint8_t *out, uint64_t out_cap, uint64_t *out_off, uint8_t *status,
+                       void *stream);
+/* Host-memory forms (device 0 of the context, synchronous). */
+int mhq_read_ints(mhq_ctx *ctx, const uint8_t *blk, uint64_t blk_len, const uint64_t *pos, const uint64_t *limit,
+                  const uint8_t *prefix, uint64_t n, int index, uint64_t *value, uint64_t *next, uint8_t *status);
+int mhq_write_ints(mhq_ctx *ctx, const uint64_t *value, const uint8_t *prefix, const uint8_t *lead, uint64_t n,
+                   uint8_t *out, uint64_t out_cap, uint64_t *out_off, uint8_t *status);
+
 #ifdef __cplusplus
 }
 #endif

@@ -23,6 +23,11 @@ MHQ_STR_OK = 0
 MHQ_STR_INVALID = 1
 MHQ_STR_EOF = 2
 MHQ_STR_NOSPACE = 3
+MHQ_INT_OK = 0
+MHQ_INT_EOF = 1
+MHQ_INT_OVERFLOW = 2
+MHQ_INT_BADARG = 3
+MHQ_INT_NOSPACE = 4
 
 u8p = C.POINTER(C.c_uint8)
 u32p = C.POINTER(C.c_uint32)
@@ -53,6 +58,10 @@ SIGNATURES = {
                                    u32p, u8p, u64p]),
     "mhq_write_strings": (C.c_int, [vp, u8p, u64p, C.c_uint64, u8p, u8p, C.c_int, u8p, C.c_uint64, u64p,
                                     u8p]),
+    "mhq_read_ints_dev": (C.c_int, [vp, C.c_int, vp, vp, vp, vp, C.c_uint64, C.c_int, vp, vp, vp, vp]),
+    "mhq_write_ints_dev": (C.c_int, [vp, C.c_int, vp, vp, vp, C.c_uint64, vp, C.c_uint64, vp, vp, vp]),
+    "mhq_read_ints": (C.c_int, [vp, u8p, C.c_uint64, u64p, u64p, u8p, C.c_uint64, C.c_int, u64p, u64p, u8p]),
+    "mhq_write_ints": (C.c_int, [vp, u64p, u8p, u8p, C.c_uint64, u8p, C.c_uint64, u64p, u8p]),
 }
 
 _lib = None

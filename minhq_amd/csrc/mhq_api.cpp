@@ -359,6 +359,25 @@ int mhq_write_strings_dev(mhq_ctx *ctx, int dev, const uint8_t *in, const uint64
                                           out_off, status, (hipStream_t)stream));
 }
 
+int mhq_read_ints_dev(mhq_ctx *ctx, int dev, const uint8_t *blk, const uint64_t *pos, const uint64_t *limit,
+                      const uint8_t *prefix, uint64_t n, int index, uint64_t *value, uint64_t *next,
+                      uint8_t *status, void *stream) {
+  Device *d = device(ctx, dev);
+  if (!d || (n && (!blk || !pos || !limit || !prefix || !value || !next || !status))) return MHQ_EINVAL;
+  MHQ_TRY(hipSetDevice(d->ordinal));
+  return hip_rc(mhq::launch_read_ints(blk, pos, limit, prefix, n, index, value, next, status, (hipStream_t)stream));
+}
+
+int mhq_write_ints_dev(mhq_ctx *ctx, int dev, const uint64_t *value, const uint8_t *prefix, const uint8_t *lead,
+                       uint64_t n, uint8_t *out, uint64_t out_cap, uint64_t *out_off, uint8_t *status,
+                       void *stream) {
+  Device *d = device(ctx, dev);
+  if (!d || !out_off || (n && (!value || !prefix || !lead || (out && !status)))) return MHQ_EINVAL;
+  MHQ_TRY(hipSetDevice(d->ordinal));
+  return hip_rc(
+      mhq::launch_write_ints(value, prefix, lead, n, out, out_cap, out_off, status, (hipStream_t)stream));
+}
+
 }  // extern "C"
 
 namespace {
@@ -441,6 +460,56 @@ int mhq_write_strings(mhq_ctx *ctx, const uint8_t *in, const uint64_t *in_off, u
   MHQ_TRY(mhq::launch_write_strings(d->tables, din.p, doff.p, n, dprefix.p, dlead.p, (uint32_t)choice,
                                     out ? dout.p : nullptr, out_cap, dout_off.p, dst.p, s));
   MHQ_TRY(dout_off.get(out_off, n + 1, s));
+  MHQ_TRY(hipStreamSynchronize(s));
+  if (out) {
+    MHQ_TRY(dout.get(out, std::min<uint64_t>(out_off[n], out_cap), s));
+    MHQ_TRY(dst.get(status, n, s));
+  }
+  return hip_rc(hipStreamSynchronize(s));
+}
+
+int mhq_read_ints(mhq_ctx *ctx, const uint8_t *blk, uint64_t blk_len, const uint64_t *pos, const uint64_t *limit,
+                  const uint8_t *prefix, uint64_t n, int index, uint64_t *value, uint64_t *next, uint8_t *status) {
+  Device *d = device(ctx, 0);
+  if (!d || (n && (!blk || !pos || !limit || !prefix || !value || !next || !status))) return MHQ_EINVAL;
+  for (uint64_t i = 0; i < n; i++)
+    if (limit[i] > blk_len) return MHQ_EINVAL;
+  std::lock_guard<std::mutex> lock(d->mu);
+  MHQ_TRY(hipSetDevice(d->ordinal));
+  hipStream_t s = d->stream;
+  DevArray<uint8_t> dblk, dprefix, dst;
+  DevArray<uint64_t> dpos, dlim, dval, dnext;
+  MHQ_TRY(dblk.put(blk, blk_len, s));
+  MHQ_TRY(dpos.put(pos, n, s));
+  MHQ_TRY(dlim.put(limit, n, s));
+  MHQ_TRY(dprefix.put(prefix, n, s));
+  MHQ_TRY(dval.alloc(n));
+  MHQ_TRY(dnext.alloc(n));
+  MHQ_TRY(dst.alloc(n));
+  MHQ_TRY(mhq::launch_read_ints(dblk.p, dpos.p, dlim.p, dprefix.p, n, index, dval.p, dnext.p, dst.p, s));
+  MHQ_TRY(dval.get(value, n, s));
+  MHQ_TRY(dnext.get(next, n, s));
+  MHQ_TRY(dst.get(status, n, s));
+  return hip_rc(hipStreamSynchronize(s));
+}
+
+int mhq_write_ints(mhq_ctx *ctx, const uint64_t *value, const uint8_t *prefix, const uint8_t *lead, uint64_t n,
+                   uint8_t *out, uint64_t out_cap, uint64_t *out_off, uint8_t *status) {
+  Device *d = device(ctx, 0);
+  if (!d || !out_off || (n && (!value || !prefix || !lead || (out && !status)))) return MHQ_EINVAL;
+  std::lock_guard<std::mutex> lock(d->mu);
+  MHQ_TRY(hipSetDevice(d->ordinal));
+  hipStream_t s = d->stream;
+  DevArray<uint8_t> dprefix, dlead, dout, dst;
+  DevArray<uint64_t> dval, doff;
+  MHQ_TRY(dval.put(value, n, s));
+  MHQ_TRY(dprefix.put(prefix, n, s));
+  MHQ_TRY(dlead.put(lead, n, s));
+  MHQ_TRY(doff.alloc(n + 1));
+  MHQ_TRY(dst.alloc(n));
+  if (out) MHQ_TRY(dout.alloc(out_cap));
+  MHQ_TRY(mhq::launch_write_ints(dval.p, dprefix.p, dlead.p, n, out ? dout.p : nullptr, out_cap, doff.p, dst.p, s));
+  MHQ_TRY(doff.get(out_off, n + 1, s));
   MHQ_TRY(hipStreamSynchronize(s));
   if (out) {
     MHQ_TRY(dout.get(out, std::min<uint64_t>(out_off[n], out_cap), s));

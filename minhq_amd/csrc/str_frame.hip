@@ -199,6 +199,97 @@ __global__ void write_frame_kernel(const uint8_t *__restrict__ in, const uint64_
   status[i] = MHQ_STR_OK;
 }
 
+// ---- prefix integers -----------------------------------
+
+// Reader.ReadInt(prefix) at byte pos, the integer's prefix in the low prefix
+// bits of that octet, reading no byte at or past limit (hc/io.go:25-55).  The
+// caller's opcode owns the bits above the prefix.  MHQ_INT_EOF where ReadBits
+// would meet the end of the block, MHQ_INT_OVERFLOW where ReadInt returns
+// ErrIntegerOverflow (hc/io.go:46); with `index` set, a value above the
+// largest int is ErrIntegerOverflow too (ReadIndex, hc/io.go:59-67).
+__global__ void read_ints_kernel(const uint8_t *__restrict__ blk, const uint64_t *__restrict__ pos,
+                                 const uint64_t *__restrict__ limit, const uint8_t *__restrict__ prefix, uint64_t n,
+                                 uint32_t index, uint64_t *__restrict__ value, uint64_t *__restrict__ next,
+                                 uint8_t *__restrict__ status) {
+  const uint64_t i = (uint64_t)blockIdx.x * kT + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t p0 = pos[i], lim = limit[i];
+  const uint32_t pf = prefix[i];
+  uint8_t st = MHQ_INT_OK;
+  uint64_t v = 0, q = p0;
+  if (pf < 1 || pf > 8) {
+    st = MHQ_INT_BADARG;
+  } else if (p0 >= lim) {
+    st = MHQ_INT_EOF;
+  } else {
+    const uint64_t mask = (1ull << pf) - 1u;
+    v = blk[q++] & mask;
+    if (v == mask) {
+      for (uint32_t s = 0; s < 64; s += 7) {
+        if (q >= lim) {
+          st = MHQ_INT_EOF;
+          break;
+        }
+        const uint64_t b = blk[q++];
+        if (s == 63 && (b > 1 || (b == 1 && (v >> 63) == 1))) {
+          st = MHQ_INT_OVERFLOW;
+          break;
+        }
+        v += (b & 0x7f) << s;
+        if ((b & 0x80) == 0) break;
+      }
+    }
+    if (st == MHQ_INT_OK && index && (v >> 63)) st = MHQ_INT_OVERFLOW;
+  }
+  value[i] = st == MHQ_INT_OK ? v : 0u;
+  next[i] = st == MHQ_INT_OK ? q : p0;
+  status[i] = st;
+}
+
+__global__ void write_ints_size_kernel(const uint64_t *__restrict__ value, const uint8_t *__restrict__ prefix,
+                                       uint64_t n, uint32_t *__restrict__ size) {
+  const uint64_t i = (uint64_t)blockIdx.x * kT + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t pf = prefix[i];
+  size[i] = pf >= 1 && pf <= 8 ? 1u + int_bytes(value[i], pf) : 0u;
+}
+
+// Writer.WriteInt(v, prefix) after the opcode bits lead[i] (hc/io.go:110-137).
+__global__ void write_ints_kernel(const uint64_t *__restrict__ value, const uint8_t *__restrict__ prefix,
+                                  const uint8_t *__restrict__ lead, uint64_t n, const uint64_t *__restrict__ out_off,
+                                  uint64_t out_cap, uint8_t *__restrict__ out, uint8_t *__restrict__ status) {
+  const uint64_t i = (uint64_t)blockIdx.x * kT + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t pf = prefix[i];
+  if (pf < 1 || pf > 8) {
+    status[i] = MHQ_INT_BADARG;
+    return;
+  }
+  if (out_off[i + 1] > out_cap) {
+    status[i] = MHQ_INT_NOSPACE;
+    return;
+  }
+  uint8_t *dst = out + out_off[i];
+  const uint64_t ones = (1ull << pf) - 1u;
+  const uint32_t b0 = pf == 8 ? 0u : ((uint32_t)lead[i] << pf);
+  uint64_t v = value[i];
+  if (v < ones) {
+    dst[0] = (uint8_t)(b0 | (uint32_t)v);
+  } else {
+    dst[0] = (uint8_t)(b0 | (uint32_t)ones);
+    v -= ones;
+    uint64_t k = 1;
+    for (bool done = false; !done;) {
+      uint32_t b = (uint32_t)(v & 0x7f);
+      v >>= 7;
+      if (v > 0) b |= 0x80;
+      else done = true;
+      dst[k++] = (uint8_t)b;
+    }
+  }
+  status[i] = MHQ_INT_OK;
+}
+
 template <class T>
 hipError_t scratch(T **p, uint64_t count, hipStream_t s) {
   return hipMallocAsync((void **)p, (count ? count : 1) * sizeof(T), s);
@@ -292,6 +383,30 @@ done:
   (void)hipFreeAsync(enc, s);
   (void)hipFreeAsync(huff, s);
   (void)base;
+  return e;
+}
+
+hipError_t launch_read_ints(const uint8_t *blk, const uint64_t *pos, const uint64_t *limit, const uint8_t *prefix,
+                            uint64_t n, int index, uint64_t *value, uint64_t *next, uint8_t *status, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  read_ints_kernel<<<blocks(n), kT, 0, s>>>(blk, pos, limit, prefix, n, index ? 1u : 0u, value, next, status);
+  return hipGetLastError();
+}
+
+hipError_t launch_write_ints(const uint64_t *value, const uint8_t *prefix, const uint8_t *lead, uint64_t n,
+                             uint8_t *out, uint64_t out_cap, uint64_t *out_off, uint8_t *status, hipStream_t s) {
+  if (n == 0) return hipMemsetAsync(out_off, 0, sizeof(uint64_t), s);
+  uint32_t *size = nullptr;
+  hipError_t e = scratch(&size, n, s);
+  if (e != hipSuccess) return e;
+  write_ints_size_kernel<<<blocks(n), kT, 0, s>>>(value, prefix, n, size);
+  e = hipGetLastError();
+  if (e == hipSuccess) e = launch_offsets(size, n, 0, out_off, nullptr, s);
+  if (e == hipSuccess && out) {
+    write_ints_kernel<<<blocks(n), kT, 0, s>>>(value, prefix, lead, n, out_off, out_cap, out, status);
+    e = hipGetLastError();
+  }
+  (void)hipFreeAsync(size, s);
   return e;
 }
 

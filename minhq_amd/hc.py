@@ -208,6 +208,47 @@ class Codec:
             raise RuntimeError("mhq_write_strings: output buffer too small")
         return unpack(out, out_off)
 
+    # ---------------- prefix integers (hc/io.go:25-67, 110-137) ---------------
+    def read_ints(self, blk: bytes, pos: Sequence[int], prefix: Sequence[int],
+                  limit: Optional[Sequence[int]] = None, index: bool = False):
+        """Batch Reader.ReadInt (ReadIndex with index=True): integer i at byte
+        pos[i], its prefix in the low prefix[i] bits, reading up to limit[i]
+        (default: the end of blk).  Returns (values, status, next) with
+        status MHQ_INT_* per integer."""
+        n = len(pos)
+        blk_a = _nonempty(np.frombuffer(bytes(blk), dtype=np.uint8).copy())
+        pos_a = _nonempty(np.ascontiguousarray(pos, dtype=np.uint64))
+        lim_a = _nonempty(np.ascontiguousarray(limit if limit is not None else [len(blk)] * n, dtype=np.uint64))
+        pf_a = _nonempty(np.ascontiguousarray(prefix, dtype=np.uint8))
+        val = np.zeros(max(n, 1), dtype=np.uint64)
+        nxt = np.zeros(max(n, 1), dtype=np.uint64)
+        status = np.zeros(max(n, 1), dtype=np.uint8)
+        check(self._L.mhq_read_ints(self._h, _p(blk_a, C.c_uint8), len(blk), _p(pos_a, C.c_uint64),
+                                    _p(lim_a, C.c_uint64), _p(pf_a, C.c_uint8), n, 1 if index else 0,
+                                    _p(val, C.c_uint64), _p(nxt, C.c_uint64), _p(status, C.c_uint8)),
+              "mhq_read_ints")
+        return [int(v) for v in val[:n]], status[:n].copy(), [int(x) for x in nxt[:n]]
+
+    def write_ints(self, values: Sequence[int], prefix: Sequence[int],
+                   lead: Optional[Sequence[int]] = None) -> List[bytes]:
+        """Batch Writer.WriteInt(v, prefix) after opcode bits lead[i]."""
+        n = len(values)
+        val_a = _nonempty(np.array([int(v) for v in values], dtype=np.uint64))
+        pf_a = _nonempty(np.ascontiguousarray(prefix, dtype=np.uint8))
+        ld_a = _nonempty(np.ascontiguousarray(lead if lead is not None else [0] * n, dtype=np.uint8))
+        out_off = np.zeros(n + 1, dtype=np.uint64)
+        check(self._L.mhq_write_ints(self._h, _p(val_a, C.c_uint64), _p(pf_a, C.c_uint8), _p(ld_a, C.c_uint8), n,
+                                     None, 0, _p(out_off, C.c_uint64), None), "mhq_write_ints (size)")
+        cap = int(out_off[-1]) if n else 0
+        out = np.zeros(max(cap, 1), dtype=np.uint8)
+        status = np.zeros(max(n, 1), dtype=np.uint8)
+        check(self._L.mhq_write_ints(self._h, _p(val_a, C.c_uint64), _p(pf_a, C.c_uint8), _p(ld_a, C.c_uint8), n,
+                                     _p(out, C.c_uint8), cap, _p(out_off, C.c_uint64), _p(status, C.c_uint8)),
+              "mhq_write_ints")
+        if n and np.any(status[:n] != _lib.MHQ_INT_OK):
+            raise ValueError("mhq_write_ints: prefix outside 1..8")
+        return unpack(out, out_off)
+
     # ---------------- device-resident batches (torch tensors on one device) ---
     @staticmethod
     def _stream(stream):
@@ -310,6 +351,34 @@ def WriteStringRawBatch(strs: Sequence[bytes], prefix: Sequence[int], choice: in
     the frame starting with opcode bits lead[i] above the H bit."""
     codec = codec or default_codec()
     return codec.write_strings(strs, prefix, lead, choice)
+
+
+class IntegerOverflow(OverflowError):
+    """ErrIntegerOverflow (hc/io.go:12)."""
+
+    def __init__(self):
+        super().__init__("integer overflow")
+
+
+def ReadIntBatch(blk: bytes, pos: Sequence[int], prefix: Sequence[int], limit: Optional[Sequence[int]] = None,
+                 index: bool = False, codec: Optional[Codec] = None):
+    """Per integer: Reader.ReadInt(prefix[i]) (ReadIndex with index=True) at
+    pos[i] (hc/io.go:25-67); returns (values, errors, next positions)."""
+    codec = codec or default_codec()
+    vals, status, nxt = codec.read_ints(blk, pos, prefix, limit, index)
+    errs: List[Optional[Exception]] = []
+    for st in status:
+        errs.append(IntegerOverflow() if st == _lib.MHQ_INT_OVERFLOW
+                    else EOFError("EOF") if st == _lib.MHQ_INT_EOF
+                    else ValueError("prefix outside 1..8") if st == _lib.MHQ_INT_BADARG else None)
+    return vals, errs, nxt
+
+
+def WriteIntBatch(values: Sequence[int], prefix: Sequence[int], lead: Optional[Sequence[int]] = None,
+                  codec: Optional[Codec] = None) -> List[bytes]:
+    """Per integer: Writer.WriteInt(v, prefix[i]) after opcode bits lead[i] (hc/io.go:110-137)."""
+    codec = codec or default_codec()
+    return codec.write_ints(values, prefix, lead)
 
 
 def HuffmanChoose(raw_len: int, enc_len: int, choice: int = HuffmanCodingAuto) -> bool:

@@ -368,6 +368,28 @@ static int br_read_int(orc_br *br, uint8_t prefix, uint64_t *out) {
   return 0;
 }
 
+/* Reader.ReadInt(prefix) after `skip_bits` opcode bits (hc/io.go:25-55):
+ * ORC_OK with *out and *consumed (whole octets read), ORC_ERR_EOF when the
+ * input ends inside the integer, ORC_ERR_OVERFLOW (hc/io.go:46). */
+int orc_read_int(const uint8_t *in, size_t len, uint8_t skip_bits, uint8_t prefix, uint64_t *out,
+                 size_t *consumed) {
+  orc_br br = {in, len, 0, 0, 0};
+  uint64_t tmp;
+  *out = 0;
+  *consumed = 0;
+  if (skip_bits) {
+    int err = br_read_bits(&br, skip_bits, &tmp);
+    if (err) return err;
+  }
+  int err = br_read_int(&br, prefix, out);
+  if (err) {
+    *out = 0;
+    return err;
+  }
+  *consumed = br.pos;
+  return ORC_OK;
+}
+
 int orc_read_string(const uint8_t *in, size_t len, uint8_t skip_bits, uint8_t prefix,
                     uint8_t *out, size_t cap, size_t *out_len, size_t *consumed) {
   orc_init();
@@ -420,6 +442,20 @@ static int bw_write_int(orc_bw *bw, uint64_t p, uint8_t prefix) {
     if (err) return err;
   }
   return 0;
+}
+
+/* Writer.WriteInt(v, prefix) after `lead_bits` opcode bits of value `lead`
+ * (hc/io.go:110-137), flushed to whole octets. */
+int orc_write_int(uint64_t v, uint8_t lead, uint8_t lead_bits, uint8_t prefix, uint8_t *out, size_t cap,
+                  size_t *out_len) {
+  orc_bw bw;
+  memset(&bw, 0, sizeof(bw));
+  bw.out = out;
+  bw.cap = cap;
+  int err = lead_bits ? bw_write_bits(&bw, lead, lead_bits) : 0;
+  if (!err) err = bw_write_int(&bw, v, prefix);
+  *out_len = bw.written;
+  return err;
 }
 
 /* WriteStringRaw: hc/io.go:153-197.  choice: 0 Auto, 1 Always, 2 Never

@@ -55,6 +55,8 @@ def lib():
         L.orc_huff_decode.argtypes = [u8p, sz, u8p, sz, szp]
         L.orc_read_string.argtypes = [u8p, sz, C.c_uint8, C.c_uint8, u8p, sz, szp, szp]
         L.orc_write_string.argtypes = [u8p, sz, C.c_uint8, C.c_uint8, C.c_uint8, C.c_int, u8p, sz, szp]
+        L.orc_read_int.argtypes = [u8p, sz, C.c_uint8, C.c_uint8, C.POINTER(C.c_uint64), szp]
+        L.orc_write_int.argtypes = [C.c_uint64, C.c_uint8, C.c_uint8, C.c_uint8, u8p, sz, szp]
         L.orc_encode_len_batch.argtypes = [u8p, u64p, C.c_uint64, u32p, C.c_int]
         L.orc_encode_batch.argtypes = [u8p, u64p, C.c_uint64, u8p, u64p, C.c_int]
         L.orc_decode_batch.argtypes = [u8p, u64p, C.c_uint64, u8p, u64p, u32p, u8p, C.c_int]
@@ -113,6 +115,26 @@ def decode(enc: bytes, cap: int | None = None):
     got = C.c_size_t(0)
     st = L.orc_huff_decode(_buf(enc), len(enc), out, cap, C.byref(got))
     return bytes(out[: got.value]), st
+
+
+def read_int(data: bytes, prefix: int, skip_bits: int = 0):
+    """Reader.ReadInt (hc/io.go:25-55) after skip_bits opcode bits:
+    returns (value, rc, consumed octets); rc 0 OK, ERR_EOF or ERR_OVERFLOW."""
+    L = lib()
+    v, used = C.c_uint64(0), C.c_size_t(0)
+    rc = L.orc_read_int(_buf(data), len(data), skip_bits, prefix, C.byref(v), C.byref(used))
+    return v.value, rc, used.value
+
+
+def write_int(v: int, prefix: int, lead: int = 0, lead_bits: int = 0) -> bytes:
+    """Writer.WriteInt (hc/io.go:110-137) after lead_bits opcode bits."""
+    L = lib()
+    out = (C.c_uint8 * 16)()
+    got = C.c_size_t(0)
+    rc = L.orc_write_int(C.c_uint64(v), lead, lead_bits, prefix, out, 16, C.byref(got))
+    if rc:
+        raise RuntimeError(f"oracle write_int rc={rc}")
+    return bytes(out[: got.value])
 
 
 def read_string(data: bytes, prefix: int = 7, skip_bits: int = 0):

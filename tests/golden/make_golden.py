@@ -13,6 +13,7 @@ Sources:
   * hc/huffmantable.go:9-267     -> huffman_table.json (256 {len, val})
   * hc/huffman_test.go:12-28     -> huffman_vectors.json (text <-> hex)
   * hc/io_test.go:76-87          -> string_vectors.json (7-bit prefix literals)
+  * hc/io_test.go:11-21, 62-67   -> int_vectors.json (prefix integers, overflows)
   * io/bitio_test.go:25-45       -> bitio_vectors.json (writer op sequence)
   * hc/testcases_test.go, hc/qpack_test.go
                                  -> embedded_literals.json: every quoted string
@@ -85,6 +86,29 @@ def string_vectors():
         if lines[i].strip() == "}":
             break
     return out
+
+
+def int_vectors():
+    """encodedIntegers (hc/io_test.go:11-21) and the overflowing encodings of
+    TestIntegerOverflow (hc/io_test.go:62-67, read with prefix 8)."""
+    lines = _read("hc/io_test.go")
+    ok, bad = [], []
+    for i, ln in enumerate(lines):
+        m = re.match(r'^\s*\{(.+?),\s*"([0-9a-f]+)",\s*(\d+)\},', ln)
+        if m:
+            expr = m.group(1).strip()
+            if expr == "^uint64(0)":
+                v = (1 << 64) - 1
+            elif expr.startswith("1 << "):
+                v = 1 << int(expr[5:])
+            else:
+                v = int(expr)
+            ok.append({"value": str(v), "hex": m.group(2), "prefix": int(m.group(3)), "src": f"hc/io_test.go:{i + 1}"})
+        m = re.match(r'^\s*"(ff[0-9a-f]+)",\s*$', ln)
+        if m:
+            bad.append({"hex": m.group(1), "prefix": 8, "src": f"hc/io_test.go:{i + 1}"})
+    assert len(ok) == 9 and len(bad) == 2, (len(ok), len(bad))
+    return {"ints": ok, "overflow": bad}
 
 
 def bitio_vectors():
@@ -164,6 +188,7 @@ def main():
         "huffman_vectors.json": huffman_vectors(),
         "string_vectors.json": string_vectors(),
         "bitio_vectors.json": bitio_vectors(),
+        "int_vectors.json": int_vectors(),
         "embedded_literals.json": embedded_literals(),
         "netbsd_qif.json": netbsd_qif(),
     }
