@@ -285,6 +285,21 @@ class Codec:
                                           cap_off.data_ptr(), out_len.data_ptr(), status.data_ptr(),
                                           self._stream(stream)), "decode_dev")
 
+    def read_strings_dev(self, blk, pos, limit, prefix, out, out_off, out_len, status, nxt, dev: int = 0,
+                         stream=None) -> None:
+        n = pos.numel()
+        check(self._L.mhq_read_strings_dev(self._h, dev, blk.data_ptr(), blk.numel(), pos.data_ptr(),
+                                           limit.data_ptr(), prefix.data_ptr(), n, out.data_ptr(), out.numel(),
+                                           out_off.data_ptr(), out_len.data_ptr(), status.data_ptr(),
+                                           nxt.data_ptr(), self._stream(stream)), "read_strings_dev")
+
+    def read_ints_dev(self, blk, pos, limit, prefix, value, nxt, status, index: bool = False, dev: int = 0,
+                      stream=None) -> None:
+        n = pos.numel()
+        check(self._L.mhq_read_ints_dev(self._h, dev, blk.data_ptr(), pos.data_ptr(), limit.data_ptr(),
+                                        prefix.data_ptr(), n, 1 if index else 0, value.data_ptr(), nxt.data_ptr(),
+                                        status.data_ptr(), self._stream(stream)), "read_ints_dev")
+
 
 _default: Optional[Codec] = None
 

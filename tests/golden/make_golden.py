@@ -20,6 +20,11 @@ Sources:
     of those files whose Huffman encoding (by the oracle) occurs, behind a
     matching H-bit/length prefix octet, inside a hex vector of the same file.
     The reference's expected bytes therefore pin these pairs.
+  * hc/statictable.go            -> static_tables.json (HPACK 1-61, QPACK 0-98 entries)
+  * hc/testcases_test.go:46-435  -> header_cases.json (header lists with their
+    HPACK block, QPACK encoder-stream updates and header block, and the
+    dynamic tables after each; decoded in order as hc/hpack_test.go:76-98 and
+    hc/qpack_test.go:591-647 do)
   * errors.log:7-241             -> netbsd_qif.json (the one surviving QIF
     header set, used as corpus text for config 3 and the 'hdr' distribution)
 """
@@ -111,6 +116,106 @@ def int_vectors():
     return {"ints": ok, "overflow": bad}
 
 
+def static_tables():
+    lines = _read("hc/statictable.go")
+    out, cur = {}, None
+    for i, ln in enumerate(lines):
+        if "hpackStaticTable = " in ln:
+            cur = out.setdefault("hpack", [])
+        elif "qpackStaticTable = " in ln:
+            cur = out.setdefault("qpack", [])
+        m = re.match(r'^\s*\{(\d+), "([^"]*)", "([^"]*)"\},', ln)
+        if m and cur is not None:
+            cur.append({"index": int(m.group(1)), "name": m.group(2), "value": m.group(3),
+                        "src": f"hc/statictable.go:{i + 1}"})
+    assert len(out["hpack"]) == 61 and out["hpack"][0]["index"] == 1, len(out["hpack"])
+    assert [e["index"] for e in out["qpack"]] == list(range(len(out["qpack"])))
+    return out
+
+
+class _GoLit:
+    """A small reader of the Go composite literals in hc/testcases_test.go
+    (strings with '+' concatenation, bools, ints, nil, keyed and unkeyed
+    elements, type prefixes such as []hc.HeaderField or &[]dynamicTableEntry)."""
+
+    TOK = re.compile(r'\s+|//[^\n]*|("(?:[^"\\]|\\.)*")|([A-Za-z_][A-Za-z0-9_.]*)|(\d+)|(.)')
+
+    def __init__(self, text):
+        self.toks = []
+        for m in self.TOK.finditer(text):
+            if m.group(1):
+                self.toks.append(("s", json.loads(m.group(1))))
+            elif m.group(2):
+                self.toks.append(("id", m.group(2)))
+            elif m.group(3):
+                self.toks.append(("n", int(m.group(3))))
+            elif m.group(4):
+                self.toks.append(("p", m.group(4)))
+        self.i = 0
+
+    def peek(self, k=0):
+        return self.toks[self.i + k] if self.i + k < len(self.toks) else (None, None)
+
+    def take(self):
+        t = self.toks[self.i]
+        self.i += 1
+        return t
+
+    def value(self):
+        kind, v = self.peek()
+        if kind == "s":
+            out = self.take()[1]
+            while self.peek() == ("p", "+"):
+                self.take()
+                out += self.take()[1]
+            return out
+        if kind == "n":
+            return self.take()[1]
+        if kind == "id" and v in ("true", "false", "nil"):
+            self.take()
+            return {"true": True, "false": False, "nil": None}[v]
+        while self.peek() != ("p", "{"):  # type prefix
+            self.take()
+        return self.composite()
+
+    def composite(self):
+        assert self.take() == ("p", "{")
+        keyed, items = {}, []
+        while self.peek() != ("p", "}"):
+            if self.peek()[0] == "id" and self.peek(1) == ("p", ":"):
+                key = self.take()[1]
+                self.take()
+                keyed[key] = self.value()
+            else:
+                items.append(self.value())
+            if self.peek() == ("p", ","):
+                self.take()
+        self.take()
+        return keyed if keyed else items
+
+
+def header_cases():
+    text = "\n".join(_read("hc/testcases_test.go"))
+    start = text.index("var testCases = []testCase")
+    line0 = text[:start].count("\n") + 1
+    lit = _GoLit(text[start + len("var testCases = []testCase"):])
+    cases = lit.composite()
+    out = []
+    for c in cases:
+        heads = [{"name": h["Name"], "value": h["Value"], "sensitive": bool(h.get("Sensitive", False))}
+                 for h in c["headers"]]
+        qt = c["qpackTable"]
+        out.append({
+            "reset": c["resetTable"], "headers": heads, "huffman": c["huffman"],
+            "hpack": c["hpack"], "hpack_table": [list(e) for e in (c["hpackTable"] or [])],
+            "qpack_updates": c["qpackUpdates"], "qpack_header": c["qpackHeader"],
+            "qpack_base": qt.get("base", 0),
+            "qpack_table": None if qt.get("entries") is None else [list(e) for e in qt["entries"]],
+        })
+    assert out and out[0]["reset"], len(out)
+    return {"src": f"hc/testcases_test.go:{line0}", "cases": out}
+
+
 def bitio_vectors():
     # io/bitio_test.go:25-45 (TestWriter): the op sequence and the expected
     # buffer after each assertion, transcribed as data.
@@ -189,6 +294,8 @@ def main():
         "string_vectors.json": string_vectors(),
         "bitio_vectors.json": bitio_vectors(),
         "int_vectors.json": int_vectors(),
+        "static_tables.json": static_tables(),
+        "header_cases.json": header_cases(),
         "embedded_literals.json": embedded_literals(),
         "netbsd_qif.json": netbsd_qif(),
     }
@@ -198,6 +305,10 @@ def main():
             f.write("\n")
         n = len(obj) if isinstance(obj, list) else len(obj.get("fields", obj.get("ops", [])))
         print(f"{name}: {n} records")
+    # the static tables are also product data (minhq_amd/headers.py loads them)
+    with open(os.path.join(REPO, "minhq_amd", "static_tables.json"), "w") as f:
+        json.dump(data["static_tables.json"], f, indent=1)
+        f.write("\n")
 
 
 if __name__ == "__main__":
