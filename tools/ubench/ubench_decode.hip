@@ -37,7 +37,7 @@ struct Smem {
   uint32_t lutL[kLut1Size];
   uint32_t lut1[kLut1Size];
   uint16_t lut2[kLut2Size];
-  uint32_t in_w[kStreamWords + 8];
+  alignas(16) uint32_t in_w[kStreamWords + 8];
   uint32_t out_w[2048];
 };
 
@@ -240,6 +240,72 @@ __device__ uint32_t run(const Smem &sm, uint32_t *out_w, uint32_t p0, uint32_t p
       if constexpr (V == 7 || V == 9) out.flush(out_w);
     }
     chk += nb + optr + out.ow;
+  } else if constexpr (V == 11 || V == 12) {
+    // lean acc+ds_or loop; refill variants: V11 reads the look-ahead word only
+    // when a refill used it; V12 keeps 64 pending bits and reads two words
+    // (ds_read_b64) every other refill.
+    const uint32_t *lutL = sm.lutL;
+    const uint32_t *w = sm.in_w;
+    const uint32_t k0 = p0 >> 5;
+    uint64_t bb = (((uint64_t)w[k0] << 32) | w[k0 + 1]) << (p0 & 31u);
+    uint32_t nb = 64u - (p0 & 31u);
+    uint32_t kw = k0 + 2u, lw = w[kw];  // V11
+    uint64_t pw = 0;                     // V12
+    uint32_t pn = 0;
+    if constexpr (V == 12) {
+      if (kw & 1u) {
+        pw = (uint64_t)w[kw] << 32;
+        pn = 32u;
+        kw += 1u;
+      } else {
+        const uint2 v = *(const uint2 *)(w + kw);
+        pw = ((uint64_t)v.x << 32) | v.y;
+        pn = 64u;
+        kw += 2u;
+      }
+    }
+    OutAcc out;
+    out.init(lane * 128u + (p0 & 3u));
+    auto refill = [&]() {
+      const bool need = nb <= 32u;
+      if constexpr (V == 11) {
+        bb |= (uint64_t)(need ? lw : 0u) << ((32u - nb) & 63u);
+        nb += need ? 32u : 0u;
+        if (need) {
+          kw += 1u;
+          lw = w[kw];
+        }
+      } else {
+        bb |= (uint64_t)(need ? (uint32_t)(pw >> 32) : 0u) << ((32u - nb) & 63u);
+        nb += need ? 32u : 0u;
+        pw = need ? pw << 32 : pw;
+        pn -= need ? 32u : 0u;
+        if (pn == 0u) {
+          const uint2 v = *(const uint2 *)(w + kw);
+          pw = ((uint64_t)v.x << 32) | v.y;
+          pn = 64u;
+          kw += 2u;
+        }
+      }
+    };
+    for (uint32_t i = 0; i < probes; i += 2) {
+#pragma unroll
+      for (int u = 0; u < 2; u++) {
+        uint32_t e = lutL[(uint32_t)(bb >> 32) >> (32 - kLut1Bits)];
+        if (u == 1 && e == 0) {
+          refill();
+          uint32_t sym = 0;
+          const uint32_t L = long_code(sm.lut2, (uint32_t)(bb >> 32), sym);
+          e = L | (8u << 8) | (sym << 16);
+        }
+        bb <<= (e & 63u);
+        nb -= e & 0xffu;
+        out.put(e >> 16, (e >> 8) & 0xffu);
+      }
+      refill();
+      out.flush(out_w);
+    }
+    chk += nb + out.ow + (uint32_t)bb;
   } else if constexpr (V == 8) {
     // two independent lean chains per lane (acc + ds_or), interleaved probe by probe
     const uint32_t *lutL = sm.lutL;
@@ -398,7 +464,7 @@ int main(int argc, char **argv) {
   CHECK(hipEventCreate(&e0));
   CHECK(hipEventCreate(&e1));
   const char *names[] = {"regbuf+ds_or", "regbuf,no-out", "regbuf+ds_or,1chk", "regbuf,2chains,no-out", "window,no-out",
-                         "lean,ds_write_b16", "lean,2x ds_write_b8", "lean,acc+ds_or", "lean,acc+ds_or,2chains", "lean,no refill read", "lean,no flush"};
+                         "lean,ds_write_b16", "lean,2x ds_write_b8", "lean,acc+ds_or", "lean,acc+ds_or,2chains", "lean,no refill read", "lean,no flush", "lean,refill read when used", "lean,refill b64"};
   // host decode for the correctness check: (len, code) -> symbol
   auto host_decode = [&](uint64_t p, int nsym, std::vector<uint8_t> &outv) {
     outv.clear();
@@ -430,10 +496,13 @@ int main(int argc, char **argv) {
       case 8: ubench<8><<<grid, block>>>(d_lutL, d_lut1, d_lut2, d_words, d_starts, starts.size(), probes, d_sink, d_cyc); break;
       case 9: ubench<9><<<grid, block>>>(d_lutL, d_lut1, d_lut2, d_words, d_starts, starts.size(), probes, d_sink, d_cyc); break;
       case 10: ubench<10><<<grid, block>>>(d_lutL, d_lut1, d_lut2, d_words, d_starts, starts.size(), probes, d_sink, d_cyc); break;
+      case 11: ubench<11><<<grid, block>>>(d_lutL, d_lut1, d_lut2, d_words, d_starts, starts.size(), probes, d_sink, d_cyc); break;
+      case 12: ubench<12><<<grid, block>>>(d_lutL, d_lut1, d_lut2, d_words, d_starts, starts.size(), probes, d_sink, d_cyc); break;
     }
   };
   // correctness of the lean variants: one wave, 24 probes per lane, compare 40 output bytes
-  for (int v = 5; v < 8; v++) {
+  for (int v = 5; v < 13; v++) {
+    if (v > 7 && v < 11) continue;
     const uint32_t save = probes;
     (void)save;
     dim3 grid1(1), block1(64);
@@ -442,6 +511,8 @@ int main(int argc, char **argv) {
       case 5: ubench<5><<<grid1, block1>>>(d_lutL, d_lut1, d_lut2, d_words, d_starts, starts.size(), pr, d_sink, d_cyc); break;
       case 6: ubench<6><<<grid1, block1>>>(d_lutL, d_lut1, d_lut2, d_words, d_starts, starts.size(), pr, d_sink, d_cyc); break;
       case 7: ubench<7><<<grid1, block1>>>(d_lutL, d_lut1, d_lut2, d_words, d_starts, starts.size(), pr, d_sink, d_cyc); break;
+      case 11: ubench<11><<<grid1, block1>>>(d_lutL, d_lut1, d_lut2, d_words, d_starts, starts.size(), pr, d_sink, d_cyc); break;
+      case 12: ubench<12><<<grid1, block1>>>(d_lutL, d_lut1, d_lut2, d_words, d_starts, starts.size(), pr, d_sink, d_cyc); break;
     }
     CHECK(hipDeviceSynchronize());
     std::vector<uint32_t> sink(1 << 20);
@@ -457,7 +528,7 @@ int main(int argc, char **argv) {
     printf("check %-22s: %s (%d byte mismatches in 64 lanes x 20 bytes)\n", names[v], bad ? "MISMATCH" : "ok", bad);
   }
   const int only_v = argc > 2 ? atoi(argv[2]) : -1, only_w = argc > 3 ? atoi(argv[3]) : 0;
-  for (int v = 7; v < 11; v++) {
+  for (int v = 7; v < 13; v++) {
     if (only_v >= 0 && v != only_v) continue;
     for (int waves : {12, 16}) {
       if (only_w && waves != only_w) continue;
