@@ -133,21 +133,30 @@ __device__ void encode_literal_global(const uint8_t *src, uint64_t nbytes, uint8
 }
 
 // Encodes staged plaintext bytes [p, e); returns the encoded bit count.
+// Per staged word: its four code lookups are issued together (bytes outside
+// [p, e) look up harmlessly and contribute nothing) and the next word is read
+// ahead, so a word costs one LDS round trip, not one per byte.
 template <bool kEmit>
 __device__ __forceinline__ uint32_t encode_one(Smem<kEmit> &sm, uint32_t p, uint32_t e, uint32_t ostart) {
   uint32_t bits = 0;
   BitOut bo;
   if (kEmit) bo.init(sm.out_w, ostart);
-  for (uint32_t q = p & ~3u; q < e; q += 4u) {
-    const uint32_t w = sm.in_w[q >> 2];
+  uint32_t q = p & ~3u;
+  uint32_t w = sm.in_w[q >> 2];
+  for (; q < e; q += 4u) {
+    const uint32_t wn = sm.in_w[(q >> 2) + 1u];  // in_w has slack words past the slice
+    uint2 c[4];
+#pragma unroll
+    for (int b = 0; b < 4; b++) c[b] = sm.code[(w >> (8 * b)) & 0xffu];
 #pragma unroll
     for (int b = 0; b < 4; b++) {
       const uint32_t x = q + (uint32_t)b;
-      uint2 c = sm.code[(w >> (8 * b)) & 0xffu];
-      if (x < p || x >= e) c = make_uint2(0u, 0u);
-      bits += c.y;
-      if (kEmit) bo.put(c.x, c.y);
+      const bool in = x >= p && x < e;
+      const uint32_t len = in ? c[b].y : 0u, code = in ? c[b].x : 0u;
+      bits += len;
+      if (kEmit) bo.put(code, len);
     }
+    w = wn;
   }
   if (kEmit) bo.finish();
   return bits;
