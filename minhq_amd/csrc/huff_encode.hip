@@ -203,10 +203,11 @@ __device__ __forceinline__ void issue_next(Next &nx, const uint8_t *__restrict__
   const uint8_t *a = in + (ic - in_bias);
   const u32x4 *src = (const u32x4 *)(a - ((uintptr_t)a & 15u));
   const uint32_t chunks = prefetch_chunks(in, in_bias, ic, iend);
+  if (chunks == 0) return;  // nothing left: the aligned chunk at the end may lie past the buffer
 #pragma unroll
   for (int k = 0; k < kPF; k++) {
-    const uint32_t c = min(tid + (uint32_t)kT * k, chunks ? chunks - 1u : 0u);
-    nx.v[k] = __builtin_nontemporal_load(src + c);  // aligned: never crosses a page
+    const uint32_t c = min(tid + (uint32_t)kT * k, chunks - 1u);
+    nx.v[k] = __builtin_nontemporal_load(src + c);  // aligned, holds a valid byte: never crosses a page
   }
 }
 

@@ -194,14 +194,9 @@ def test_unaligned_offsets_and_bias(codec, oracle_mod):
         assert out[a: a + int(out_len[i])].tobytes() == x
 
 
-def test_device_resident_round_trip_full_size(codec):
-    """Config 2 at full size (2^20 literals) through the device entry points:
-    encode -> offsets -> decode reproduces the plaintext exactly."""
+def _device_round_trip(codec, b):
     import torch
 
-    from minhq_amd import workloads
-
-    b = workloads.config2()
     dev = torch.device("cuda:0")
     data = torch.from_numpy(b.data).to(dev)
     off = torch.from_numpy(b.off.view(np.int64)).to(dev)
@@ -233,3 +228,20 @@ def test_device_resident_round_trip_full_size(codec):
     codec.capacity_dev(enc_off, cap2)
     torch.cuda.synchronize()
     assert torch.equal(cap2, cap_off)
+
+
+def test_device_resident_round_trip_full_size(codec):
+    """Config 2 at full size (2^20 literals) through the device entry points:
+    encode -> offsets -> decode reproduces the plaintext exactly."""
+    from minhq_amd import workloads
+
+    _device_round_trip(codec, workloads.config2())
+
+
+def test_device_resident_round_trip_adversarial_page_aligned(codec):
+    """Config 5's literals (128 B of >= 26-bit codes) at 2^20: the plaintext
+    buffer ends exactly on a page (and allocation) boundary, so any read
+    past the last literal faults."""
+    from minhq_amd import workloads
+
+    _device_round_trip(codec, workloads.config5(1 << 20))
