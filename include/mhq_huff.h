@@ -195,6 +195,38 @@ int mhq_read_ints(mhq_ctx *ctx, const uint8_t *blk, uint64_t blk_len, const uint
 int mhq_write_ints(mhq_ctx *ctx, const uint64_t *value, const uint8_t *prefix, const uint8_t *lead, uint64_t n,
                    uint8_t *out, uint64_t out_cap, uint64_t *out_off, uint8_t *status);
 
+/* ---------------- HTTP/3 (draft) frame varints -----------------------------
+ * Batch frameReader.ReadVarint / ReadFrame's header and frameWriter.WriteVarint
+ * (frame.go:72-92, 128-152): a 2-bit length code (1, 2, 4 or 8 octets), then
+ * the value MSB first; a frame header is the payload length as a varint and a
+ * type octet. */
+#define MHQ_VARINT_OK 0
+#define MHQ_VARINT_EOF 1       /* the block ended inside the varint (or before a frame's type octet) */
+#define MHQ_VARINT_TOO_LARGE 2 /* write: value >= 2^62, ErrTooLarge (frame.go:52,131-132) */
+#define MHQ_VARINT_NOSPACE 3   /* write: past out_cap (not a reference outcome) */
+
+/* Varint i at byte pos[i], reading no byte at or past limit[i]: value[i],
+ * next[i] (pos[i] on EOF), status[i].  Device pointers, async on `stream`. */
+int mhq_read_varints_dev(mhq_ctx *ctx, int dev, const uint8_t *blk, const uint64_t *pos, const uint64_t *limit,
+                         uint64_t n, uint64_t *value, uint64_t *next, uint8_t *status, void *stream);
+/* Frame header i at byte pos[i]: type[i], payload_len[i] (as declared),
+ * payload_pos[i] (the byte after the type octet; pos[i] on EOF), status[i]. */
+int mhq_read_frames_dev(mhq_ctx *ctx, int dev, const uint8_t *blk, const uint64_t *pos, const uint64_t *limit,
+                        uint64_t n, uint8_t *type, uint64_t *payload_len, uint64_t *payload_pos, uint8_t *status,
+                        void *stream);
+/* Writes value[i] as the shortest varint, back to back: varint i is
+ * out[out_off[i] .. out_off[i+1]) (empty for a value >= 2^62, status
+ * MHQ_VARINT_TOO_LARGE).  out NULL: out_off only (size query). */
+int mhq_write_varints_dev(mhq_ctx *ctx, int dev, const uint64_t *value, uint64_t n, uint8_t *out, uint64_t out_cap,
+                          uint64_t *out_off, uint8_t *status, void *stream);
+/* Host-memory forms (device 0 of the context, synchronous). */
+int mhq_read_varints(mhq_ctx *ctx, const uint8_t *blk, uint64_t blk_len, const uint64_t *pos, const uint64_t *limit,
+                     uint64_t n, uint64_t *value, uint64_t *next, uint8_t *status);
+int mhq_read_frames(mhq_ctx *ctx, const uint8_t *blk, uint64_t blk_len, const uint64_t *pos, const uint64_t *limit,
+                    uint64_t n, uint8_t *type, uint64_t *payload_len, uint64_t *payload_pos, uint8_t *status);
+int mhq_write_varints(mhq_ctx *ctx, const uint64_t *value, uint64_t n, uint8_t *out, uint64_t out_cap,
+                      uint64_t *out_off, uint8_t *status);
+
 #ifdef __cplusplus
 }
 #endif

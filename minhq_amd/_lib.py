@@ -28,6 +28,10 @@ MHQ_INT_EOF = 1
 MHQ_INT_OVERFLOW = 2
 MHQ_INT_BADARG = 3
 MHQ_INT_NOSPACE = 4
+MHQ_VARINT_OK = 0
+MHQ_VARINT_EOF = 1
+MHQ_VARINT_TOO_LARGE = 2
+MHQ_VARINT_NOSPACE = 3
 
 u8p = C.POINTER(C.c_uint8)
 u32p = C.POINTER(C.c_uint32)
@@ -62,6 +66,12 @@ SIGNATURES = {
     "mhq_write_ints_dev": (C.c_int, [vp, C.c_int, vp, vp, vp, C.c_uint64, vp, C.c_uint64, vp, vp, vp]),
     "mhq_read_ints": (C.c_int, [vp, u8p, C.c_uint64, u64p, u64p, u8p, C.c_uint64, C.c_int, u64p, u64p, u8p]),
     "mhq_write_ints": (C.c_int, [vp, u64p, u8p, u8p, C.c_uint64, u8p, C.c_uint64, u64p, u8p]),
+    "mhq_read_varints_dev": (C.c_int, [vp, C.c_int, vp, vp, vp, C.c_uint64, vp, vp, vp, vp]),
+    "mhq_read_frames_dev": (C.c_int, [vp, C.c_int, vp, vp, vp, C.c_uint64, vp, vp, vp, vp, vp]),
+    "mhq_write_varints_dev": (C.c_int, [vp, C.c_int, vp, C.c_uint64, vp, C.c_uint64, vp, vp, vp]),
+    "mhq_read_varints": (C.c_int, [vp, u8p, C.c_uint64, u64p, u64p, C.c_uint64, u64p, u64p, u8p]),
+    "mhq_read_frames": (C.c_int, [vp, u8p, C.c_uint64, u64p, u64p, C.c_uint64, u8p, u64p, u64p, u8p]),
+    "mhq_write_varints": (C.c_int, [vp, u64p, C.c_uint64, u8p, C.c_uint64, u64p, u8p]),
 }
 
 _lib = None

@@ -45,6 +45,14 @@ hipError_t launch_read_ints(const uint8_t *blk, const uint64_t *pos, const uint6
                             uint64_t n, int index, uint64_t *value, uint64_t *next, uint8_t *status, hipStream_t s);
 hipError_t launch_write_ints(const uint64_t *value, const uint8_t *prefix, const uint8_t *lead, uint64_t n,
                              uint8_t *out, uint64_t out_cap, uint64_t *out_off, uint8_t *status, hipStream_t s);
+// Batch HTTP/3 (draft) varints and frame headers (str_frame.hip); see include/mhq_huff.h.
+hipError_t launch_read_varints(const uint8_t *blk, const uint64_t *pos, const uint64_t *limit, uint64_t n,
+                               uint64_t *value, uint64_t *next, uint8_t *status, hipStream_t s);
+hipError_t launch_read_frames(const uint8_t *blk, const uint64_t *pos, const uint64_t *limit, uint64_t n,
+                              uint8_t *type, uint64_t *payload_len, uint64_t *payload_pos, uint8_t *status,
+                              hipStream_t s);
+hipError_t launch_write_varints(const uint64_t *value, uint64_t n, uint8_t *out, uint64_t out_cap,
+                                uint64_t *out_off, uint8_t *status, hipStream_t s);
 hipError_t launch_capacity(const uint64_t *in_off, uint64_t n, uint64_t base, uint64_t *cap_off,
                            hipStream_t s);
 

@@ -378,6 +378,32 @@ int mhq_write_ints_dev(mhq_ctx *ctx, int dev, const uint64_t *value, const uint8
       mhq::launch_write_ints(value, prefix, lead, n, out, out_cap, out_off, status, (hipStream_t)stream));
 }
 
+int mhq_read_varints_dev(mhq_ctx *ctx, int dev, const uint8_t *blk, const uint64_t *pos, const uint64_t *limit,
+                         uint64_t n, uint64_t *value, uint64_t *next, uint8_t *status, void *stream) {
+  Device *d = device(ctx, dev);
+  if (!d || (n && (!blk || !pos || !limit || !value || !next || !status))) return MHQ_EINVAL;
+  MHQ_TRY(hipSetDevice(d->ordinal));
+  return hip_rc(mhq::launch_read_varints(blk, pos, limit, n, value, next, status, (hipStream_t)stream));
+}
+
+int mhq_read_frames_dev(mhq_ctx *ctx, int dev, const uint8_t *blk, const uint64_t *pos, const uint64_t *limit,
+                        uint64_t n, uint8_t *type, uint64_t *payload_len, uint64_t *payload_pos, uint8_t *status,
+                        void *stream) {
+  Device *d = device(ctx, dev);
+  if (!d || (n && (!blk || !pos || !limit || !type || !payload_len || !payload_pos || !status))) return MHQ_EINVAL;
+  MHQ_TRY(hipSetDevice(d->ordinal));
+  return hip_rc(mhq::launch_read_frames(blk, pos, limit, n, type, payload_len, payload_pos, status,
+                                        (hipStream_t)stream));
+}
+
+int mhq_write_varints_dev(mhq_ctx *ctx, int dev, const uint64_t *value, uint64_t n, uint8_t *out, uint64_t out_cap,
+                          uint64_t *out_off, uint8_t *status, void *stream) {
+  Device *d = device(ctx, dev);
+  if (!d || !out_off || (n && (!value || (out && !status)))) return MHQ_EINVAL;
+  MHQ_TRY(hipSetDevice(d->ordinal));
+  return hip_rc(mhq::launch_write_varints(value, n, out, out_cap, out_off, status, (hipStream_t)stream));
+}
+
 }  // extern "C"
 
 namespace {
@@ -509,6 +535,79 @@ int mhq_write_ints(mhq_ctx *ctx, const uint64_t *value, const uint8_t *prefix, c
   MHQ_TRY(dst.alloc(n));
   if (out) MHQ_TRY(dout.alloc(out_cap));
   MHQ_TRY(mhq::launch_write_ints(dval.p, dprefix.p, dlead.p, n, out ? dout.p : nullptr, out_cap, doff.p, dst.p, s));
+  MHQ_TRY(doff.get(out_off, n + 1, s));
+  MHQ_TRY(hipStreamSynchronize(s));
+  if (out) {
+    MHQ_TRY(dout.get(out, std::min<uint64_t>(out_off[n], out_cap), s));
+    MHQ_TRY(dst.get(status, n, s));
+  }
+  return hip_rc(hipStreamSynchronize(s));
+}
+
+int mhq_read_varints(mhq_ctx *ctx, const uint8_t *blk, uint64_t blk_len, const uint64_t *pos, const uint64_t *limit,
+                     uint64_t n, uint64_t *value, uint64_t *next, uint8_t *status) {
+  Device *d = device(ctx, 0);
+  if (!d || (n && (!blk || !pos || !limit || !value || !next || !status))) return MHQ_EINVAL;
+  for (uint64_t i = 0; i < n; i++)
+    if (limit[i] > blk_len) return MHQ_EINVAL;
+  std::lock_guard<std::mutex> lock(d->mu);
+  MHQ_TRY(hipSetDevice(d->ordinal));
+  hipStream_t s = d->stream;
+  DevArray<uint8_t> dblk, dst;
+  DevArray<uint64_t> dpos, dlim, dval, dnext;
+  MHQ_TRY(dblk.put(blk, blk_len, s));
+  MHQ_TRY(dpos.put(pos, n, s));
+  MHQ_TRY(dlim.put(limit, n, s));
+  MHQ_TRY(dval.alloc(n));
+  MHQ_TRY(dnext.alloc(n));
+  MHQ_TRY(dst.alloc(n));
+  MHQ_TRY(mhq::launch_read_varints(dblk.p, dpos.p, dlim.p, n, dval.p, dnext.p, dst.p, s));
+  MHQ_TRY(dval.get(value, n, s));
+  MHQ_TRY(dnext.get(next, n, s));
+  MHQ_TRY(dst.get(status, n, s));
+  return hip_rc(hipStreamSynchronize(s));
+}
+
+int mhq_read_frames(mhq_ctx *ctx, const uint8_t *blk, uint64_t blk_len, const uint64_t *pos, const uint64_t *limit,
+                    uint64_t n, uint8_t *type, uint64_t *payload_len, uint64_t *payload_pos, uint8_t *status) {
+  Device *d = device(ctx, 0);
+  if (!d || (n && (!blk || !pos || !limit || !type || !payload_len || !payload_pos || !status))) return MHQ_EINVAL;
+  for (uint64_t i = 0; i < n; i++)
+    if (limit[i] > blk_len) return MHQ_EINVAL;
+  std::lock_guard<std::mutex> lock(d->mu);
+  MHQ_TRY(hipSetDevice(d->ordinal));
+  hipStream_t s = d->stream;
+  DevArray<uint8_t> dblk, dtype, dst;
+  DevArray<uint64_t> dpos, dlim, dlen, dppos;
+  MHQ_TRY(dblk.put(blk, blk_len, s));
+  MHQ_TRY(dpos.put(pos, n, s));
+  MHQ_TRY(dlim.put(limit, n, s));
+  MHQ_TRY(dtype.alloc(n));
+  MHQ_TRY(dlen.alloc(n));
+  MHQ_TRY(dppos.alloc(n));
+  MHQ_TRY(dst.alloc(n));
+  MHQ_TRY(mhq::launch_read_frames(dblk.p, dpos.p, dlim.p, n, dtype.p, dlen.p, dppos.p, dst.p, s));
+  MHQ_TRY(dtype.get(type, n, s));
+  MHQ_TRY(dlen.get(payload_len, n, s));
+  MHQ_TRY(dppos.get(payload_pos, n, s));
+  MHQ_TRY(dst.get(status, n, s));
+  return hip_rc(hipStreamSynchronize(s));
+}
+
+int mhq_write_varints(mhq_ctx *ctx, const uint64_t *value, uint64_t n, uint8_t *out, uint64_t out_cap,
+                      uint64_t *out_off, uint8_t *status) {
+  Device *d = device(ctx, 0);
+  if (!d || !out_off || (n && (!value || (out && !status)))) return MHQ_EINVAL;
+  std::lock_guard<std::mutex> lock(d->mu);
+  MHQ_TRY(hipSetDevice(d->ordinal));
+  hipStream_t s = d->stream;
+  DevArray<uint8_t> dout, dst;
+  DevArray<uint64_t> dval, doff;
+  MHQ_TRY(dval.put(value, n, s));
+  MHQ_TRY(doff.alloc(n + 1));
+  MHQ_TRY(dst.alloc(n));
+  if (out) MHQ_TRY(dout.alloc(out_cap));
+  MHQ_TRY(mhq::launch_write_varints(dval.p, n, out ? dout.p : nullptr, out_cap, doff.p, dst.p, s));
   MHQ_TRY(doff.get(out_off, n + 1, s));
   MHQ_TRY(hipStreamSynchronize(s));
   if (out) {

@@ -290,6 +290,94 @@ __global__ void write_ints_kernel(const uint64_t *__restrict__ value, const uint
   status[i] = MHQ_INT_OK;
 }
 
+// ---- HTTP/3 (draft) frame varints ---------------------
+
+// ReadVarint at byte pos (frame.go:72-79): the top two bits of the first
+// octet give the length (1, 2, 4 or 8 octets), the rest is the value, MSB
+// first.  MHQ_VARINT_EOF where ReadBits meets the end of the block.
+__device__ __forceinline__ uint8_t read_varint_at(const uint8_t *__restrict__ blk, uint64_t p0, uint64_t lim,
+                                                  uint64_t &v, uint64_t &q) {
+  v = 0;
+  q = p0;
+  if (p0 >= lim) return MHQ_VARINT_EOF;
+  const uint32_t b0 = blk[p0];
+  const uint32_t nb = 1u << (b0 >> 6);
+  if (p0 + nb > lim) return MHQ_VARINT_EOF;
+  uint64_t x = b0 & 0x3fu;
+  for (uint32_t k = 1; k < nb; k++) x = (x << 8) | blk[p0 + k];
+  v = x;
+  q = p0 + nb;
+  return MHQ_VARINT_OK;
+}
+
+__global__ void read_varints_kernel(const uint8_t *__restrict__ blk, const uint64_t *__restrict__ pos,
+                                    const uint64_t *__restrict__ limit, uint64_t n, uint64_t *__restrict__ value,
+                                    uint64_t *__restrict__ next, uint8_t *__restrict__ status) {
+  const uint64_t i = (uint64_t)blockIdx.x * kT + threadIdx.x;
+  if (i >= n) return;
+  uint64_t v, q;
+  status[i] = read_varint_at(blk, pos[i], limit[i], v, q);
+  value[i] = v;
+  next[i] = q;
+}
+
+// ReadFrame's header (frame.go:81-92): the payload length as a varint, then
+// the type octet; the payload is the next `len` octets.
+__global__ void read_frames_kernel(const uint8_t *__restrict__ blk, const uint64_t *__restrict__ pos,
+                                   const uint64_t *__restrict__ limit, uint64_t n, uint8_t *__restrict__ type,
+                                   uint64_t *__restrict__ payload_len, uint64_t *__restrict__ payload_pos,
+                                   uint8_t *__restrict__ status) {
+  const uint64_t i = (uint64_t)blockIdx.x * kT + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t lim = limit[i];
+  uint64_t v, q;
+  uint8_t st = read_varint_at(blk, pos[i], lim, v, q);
+  uint8_t t = 0;
+  if (st == MHQ_VARINT_OK) {
+    if (q >= lim) {
+      st = MHQ_VARINT_EOF;
+      v = 0;
+    } else {
+      t = blk[q++];
+    }
+  }
+  type[i] = t;
+  payload_len[i] = st == MHQ_VARINT_OK ? v : 0u;
+  payload_pos[i] = st == MHQ_VARINT_OK ? q : pos[i];
+  status[i] = st;
+}
+
+// WriteVarint (frame.go:128-152): the shortest of 1, 2, 4, 8 octets;
+// values >= 2^62 are ErrTooLarge (no octets).
+__global__ void write_varints_size_kernel(const uint64_t *__restrict__ value, uint64_t n, uint32_t *__restrict__ size) {
+  const uint64_t i = (uint64_t)blockIdx.x * kT + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t v = value[i];
+  size[i] = v >= (1ull << 62) ? 0u : v >= (1ull << 30) ? 8u : v >= (1ull << 14) ? 4u : v >= (1ull << 6) ? 2u : 1u;
+}
+
+__global__ void write_varints_kernel(const uint64_t *__restrict__ value, uint64_t n,
+                                     const uint64_t *__restrict__ out_off, uint64_t out_cap,
+                                     uint8_t *__restrict__ out, uint8_t *__restrict__ status) {
+  const uint64_t i = (uint64_t)blockIdx.x * kT + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t v = value[i];
+  if (v >= (1ull << 62)) {
+    status[i] = MHQ_VARINT_TOO_LARGE;
+    return;
+  }
+  if (out_off[i + 1] > out_cap) {
+    status[i] = MHQ_VARINT_NOSPACE;
+    return;
+  }
+  const uint32_t nb = (uint32_t)(out_off[i + 1] - out_off[i]);
+  const uint64_t code = nb == 8 ? 3u : nb == 4 ? 2u : nb == 2 ? 1u : 0u;
+  const uint64_t x = v | (code << (8u * nb - 2u));
+  uint8_t *dst = out + out_off[i];
+  for (uint32_t k = 0; k < nb; k++) dst[k] = (uint8_t)(x >> (8u * (nb - 1u - k)));
+  status[i] = MHQ_VARINT_OK;
+}
+
 template <class T>
 hipError_t scratch(T **p, uint64_t count, hipStream_t s) {
   return hipMallocAsync((void **)p, (count ? count : 1) * sizeof(T), s);
@@ -404,6 +492,38 @@ hipError_t launch_write_ints(const uint64_t *value, const uint8_t *prefix, const
   if (e == hipSuccess) e = launch_offsets(size, n, 0, out_off, nullptr, s);
   if (e == hipSuccess && out) {
     write_ints_kernel<<<blocks(n), kT, 0, s>>>(value, prefix, lead, n, out_off, out_cap, out, status);
+    e = hipGetLastError();
+  }
+  (void)hipFreeAsync(size, s);
+  return e;
+}
+
+hipError_t launch_read_varints(const uint8_t *blk, const uint64_t *pos, const uint64_t *limit, uint64_t n,
+                               uint64_t *value, uint64_t *next, uint8_t *status, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  read_varints_kernel<<<blocks(n), kT, 0, s>>>(blk, pos, limit, n, value, next, status);
+  return hipGetLastError();
+}
+
+hipError_t launch_read_frames(const uint8_t *blk, const uint64_t *pos, const uint64_t *limit, uint64_t n,
+                              uint8_t *type, uint64_t *payload_len, uint64_t *payload_pos, uint8_t *status,
+                              hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  read_frames_kernel<<<blocks(n), kT, 0, s>>>(blk, pos, limit, n, type, payload_len, payload_pos, status);
+  return hipGetLastError();
+}
+
+hipError_t launch_write_varints(const uint64_t *value, uint64_t n, uint8_t *out, uint64_t out_cap,
+                                uint64_t *out_off, uint8_t *status, hipStream_t s) {
+  if (n == 0) return hipMemsetAsync(out_off, 0, sizeof(uint64_t), s);
+  uint32_t *size = nullptr;
+  hipError_t e = scratch(&size, n, s);
+  if (e != hipSuccess) return e;
+  write_varints_size_kernel<<<blocks(n), kT, 0, s>>>(value, n, size);
+  e = hipGetLastError();
+  if (e == hipSuccess) e = launch_offsets(size, n, 0, out_off, nullptr, s);
+  if (e == hipSuccess && out) {
+    write_varints_kernel<<<blocks(n), kT, 0, s>>>(value, n, out_off, out_cap, out, status);
     e = hipGetLastError();
   }
   (void)hipFreeAsync(size, s);

@@ -249,6 +249,53 @@ class Codec:
             raise ValueError("mhq_write_ints: prefix outside 1..8")
         return unpack(out, out_off)
 
+    # ---------------- HTTP/3 (draft) frame varints (frame.go:72-92, 128-152) --
+    def _blk_args(self, blk, pos, limit):
+        n = len(pos)
+        blk_a = _nonempty(np.frombuffer(bytes(blk), dtype=np.uint8).copy())
+        pos_a = _nonempty(np.ascontiguousarray(pos, dtype=np.uint64))
+        lim_a = _nonempty(np.ascontiguousarray(limit if limit is not None else [len(blk)] * n, dtype=np.uint64))
+        return n, blk_a, pos_a, lim_a
+
+    def read_varints(self, blk: bytes, pos: Sequence[int], limit: Optional[Sequence[int]] = None):
+        """Batch frameReader.ReadVarint: (values, status, next), status MHQ_VARINT_*."""
+        n, blk_a, pos_a, lim_a = self._blk_args(blk, pos, limit)
+        val = np.zeros(max(n, 1), dtype=np.uint64)
+        nxt = np.zeros(max(n, 1), dtype=np.uint64)
+        st = np.zeros(max(n, 1), dtype=np.uint8)
+        check(self._L.mhq_read_varints(self._h, _p(blk_a, C.c_uint8), len(blk), _p(pos_a, C.c_uint64),
+                                       _p(lim_a, C.c_uint64), n, _p(val, C.c_uint64), _p(nxt, C.c_uint64),
+                                       _p(st, C.c_uint8)), "mhq_read_varints")
+        return [int(v) for v in val[:n]], st[:n].copy(), [int(x) for x in nxt[:n]]
+
+    def read_frames(self, blk: bytes, pos: Sequence[int], limit: Optional[Sequence[int]] = None):
+        """Batch ReadFrame headers: (types, payload lengths, payload positions, status)."""
+        n, blk_a, pos_a, lim_a = self._blk_args(blk, pos, limit)
+        typ = np.zeros(max(n, 1), dtype=np.uint8)
+        plen = np.zeros(max(n, 1), dtype=np.uint64)
+        ppos = np.zeros(max(n, 1), dtype=np.uint64)
+        st = np.zeros(max(n, 1), dtype=np.uint8)
+        check(self._L.mhq_read_frames(self._h, _p(blk_a, C.c_uint8), len(blk), _p(pos_a, C.c_uint64),
+                                      _p(lim_a, C.c_uint64), n, _p(typ, C.c_uint8), _p(plen, C.c_uint64),
+                                      _p(ppos, C.c_uint64), _p(st, C.c_uint8)), "mhq_read_frames")
+        return ([int(t) for t in typ[:n]], [int(x) for x in plen[:n]], [int(x) for x in ppos[:n]],
+                st[:n].copy())
+
+    def write_varints(self, values: Sequence[int]):
+        """Batch frameWriter.WriteVarint: (encodings, status); a value >= 2^62
+        gives b"" and MHQ_VARINT_TOO_LARGE (ErrTooLarge)."""
+        n = len(values)
+        val_a = _nonempty(np.array([int(v) for v in values], dtype=np.uint64))
+        out_off = np.zeros(n + 1, dtype=np.uint64)
+        check(self._L.mhq_write_varints(self._h, _p(val_a, C.c_uint64), n, None, 0, _p(out_off, C.c_uint64), None),
+              "mhq_write_varints (size)")
+        cap = int(out_off[-1]) if n else 0
+        out = np.zeros(max(cap, 1), dtype=np.uint8)
+        st = np.zeros(max(n, 1), dtype=np.uint8)
+        check(self._L.mhq_write_varints(self._h, _p(val_a, C.c_uint64), n, _p(out, C.c_uint8), cap,
+                                        _p(out_off, C.c_uint64), _p(st, C.c_uint8)), "mhq_write_varints")
+        return unpack(out, out_off), st[:n].copy()
+
     # ---------------- device-resident batches (torch tensors on one device) ---
     @staticmethod
     def _stream(stream):
@@ -299,6 +346,12 @@ class Codec:
         check(self._L.mhq_read_ints_dev(self._h, dev, blk.data_ptr(), pos.data_ptr(), limit.data_ptr(),
                                         prefix.data_ptr(), n, 1 if index else 0, value.data_ptr(), nxt.data_ptr(),
                                         status.data_ptr(), self._stream(stream)), "read_ints_dev")
+
+    def read_varints_dev(self, blk, pos, limit, value, nxt, status, dev: int = 0, stream=None) -> None:
+        n = pos.numel()
+        check(self._L.mhq_read_varints_dev(self._h, dev, blk.data_ptr(), pos.data_ptr(), limit.data_ptr(), n,
+                                           value.data_ptr(), nxt.data_ptr(), status.data_ptr(),
+                                           self._stream(stream)), "read_varints_dev")
 
 
 _default: Optional[Codec] = None

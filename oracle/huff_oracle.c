@@ -458,6 +458,66 @@ int orc_write_int(uint64_t v, uint8_t lead, uint8_t lead_bits, uint8_t prefix, u
   return err;
 }
 
+/* ------------------------------------------------------------------------ */
+/* HTTP/3 (draft) frame varints (frame.go:72-92, 128-152).                   */
+/* ------------------------------------------------------------------------ */
+
+/* ReadVarint (frame.go:72-79): a 2-bit length code, then (8 << code) - 2
+ * value bits, MSB first. */
+int orc_read_varint(const uint8_t *in, size_t len, uint64_t *out, size_t *consumed) {
+  orc_br br = {in, len, 0, 0, 0};
+  uint64_t code;
+  *out = 0;
+  *consumed = 0;
+  int err = br_read_bits(&br, 2, &code);
+  if (err) return err;
+  err = br_read_bits(&br, (uint8_t)((8u << code) - 2u), out);
+  if (err) {
+    *out = 0;
+    return err;
+  }
+  *consumed = br.pos;
+  return ORC_OK;
+}
+
+/* WriteVarint (frame.go:128-152): the shortest of 1, 2, 4, 8 octets;
+ * values >= 2^62 are ErrTooLarge. */
+int orc_write_varint(uint64_t v, uint8_t *out, size_t cap, size_t *out_len) {
+  orc_bw bw;
+  memset(&bw, 0, sizeof(bw));
+  bw.out = out;
+  bw.cap = cap;
+  *out_len = 0;
+  uint8_t size;
+  if (v >= (1ull << 62)) return ORC_ERR_TOO_LARGE;
+  if (v >= (1ull << 30)) size = 3;
+  else if (v >= (1ull << 14)) size = 2;
+  else if (v >= (1ull << 6)) size = 1;
+  else size = 0;
+  int err = bw_write_bits(&bw, size, 2);
+  if (!err) err = bw_write_bits(&bw, v, (uint8_t)((1u << size) * 8u - 2u));
+  *out_len = bw.written;
+  return err;
+}
+
+/* ReadFrame's header (frame.go:81-92): the payload length as a varint, then
+ * the type octet; the payload is the next `len` octets (a LimitedReader). */
+int orc_read_frame(const uint8_t *in, size_t len, uint8_t *type, uint64_t *plen, size_t *hdr_len) {
+  size_t used = 0;
+  *type = 0;
+  *plen = 0;
+  *hdr_len = 0;
+  int err = orc_read_varint(in, len, plen, &used);
+  if (err) return err;
+  if (used >= len) {
+    *plen = 0;
+    return ORC_ERR_EOF;
+  }
+  *type = in[used];
+  *hdr_len = used + 1;
+  return ORC_OK;
+}
+
 /* WriteStringRaw: hc/io.go:153-197.  choice: 0 Auto, 1 Always, 2 Never
  * (hc/io.go:140-150).  Writes H bit + prefix integer + payload starting on an
  * octet boundary after `lead_bits` opcode bits (value `lead`). */

@@ -37,6 +37,9 @@ int orc_read_int(const uint8_t *in, size_t len, uint8_t skip_bits, uint8_t prefi
                  size_t *consumed);
 int orc_write_int(uint64_t v, uint8_t lead, uint8_t lead_bits, uint8_t prefix, uint8_t *out, size_t cap,
                   size_t *out_len);
+int orc_read_varint(const uint8_t *in, size_t len, uint64_t *out, size_t *consumed);
+int orc_write_varint(uint64_t v, uint8_t *out, size_t cap, size_t *out_len);
+int orc_read_frame(const uint8_t *in, size_t len, uint8_t *type, uint64_t *plen, size_t *hdr_len);
 int orc_read_string(const uint8_t *in, size_t len, uint8_t skip_bits, uint8_t prefix,
                     uint8_t *out, size_t cap, size_t *out_len, size_t *consumed);
 int orc_write_string(const uint8_t *s, size_t len, uint8_t lead, uint8_t lead_bits,

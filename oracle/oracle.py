@@ -56,6 +56,9 @@ def lib():
         L.orc_read_string.argtypes = [u8p, sz, C.c_uint8, C.c_uint8, u8p, sz, szp, szp]
         L.orc_write_string.argtypes = [u8p, sz, C.c_uint8, C.c_uint8, C.c_uint8, C.c_int, u8p, sz, szp]
         L.orc_read_int.argtypes = [u8p, sz, C.c_uint8, C.c_uint8, C.POINTER(C.c_uint64), szp]
+        L.orc_read_varint.argtypes = [u8p, sz, C.POINTER(C.c_uint64), szp]
+        L.orc_write_varint.argtypes = [C.c_uint64, u8p, sz, szp]
+        L.orc_read_frame.argtypes = [u8p, sz, C.POINTER(C.c_uint8), C.POINTER(C.c_uint64), szp]
         L.orc_write_int.argtypes = [C.c_uint64, C.c_uint8, C.c_uint8, C.c_uint8, u8p, sz, szp]
         L.orc_encode_len_batch.argtypes = [u8p, u64p, C.c_uint64, u32p, C.c_int]
         L.orc_encode_batch.argtypes = [u8p, u64p, C.c_uint64, u8p, u64p, C.c_int]
@@ -135,6 +138,31 @@ def write_int(v: int, prefix: int, lead: int = 0, lead_bits: int = 0) -> bytes:
     if rc:
         raise RuntimeError(f"oracle write_int rc={rc}")
     return bytes(out[: got.value])
+
+
+def read_varint(data: bytes):
+    """ReadVarint (frame.go:72-79): (value, rc, consumed)."""
+    L = lib()
+    v, used = C.c_uint64(0), C.c_size_t(0)
+    rc = L.orc_read_varint(_buf(data), len(data), C.byref(v), C.byref(used))
+    return v.value, rc, used.value
+
+
+def write_varint(v: int):
+    """WriteVarint (frame.go:128-152): (bytes, rc); rc ERR_TOO_LARGE for v >= 2^62."""
+    L = lib()
+    out = (C.c_uint8 * 8)()
+    got = C.c_size_t(0)
+    rc = L.orc_write_varint(C.c_uint64(v), out, 8, C.byref(got))
+    return bytes(out[: got.value]), rc
+
+
+def read_frame(data: bytes):
+    """ReadFrame's header (frame.go:81-92): (type, payload length, header length, rc)."""
+    L = lib()
+    t, pl, hl = C.c_uint8(0), C.c_uint64(0), C.c_size_t(0)
+    rc = L.orc_read_frame(_buf(data), len(data), C.byref(t), C.byref(pl), C.byref(hl))
+    return t.value, pl.value, hl.value, rc
 
 
 def read_string(data: bytes, prefix: int = 7, skip_bits: int = 0):

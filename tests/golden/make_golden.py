@@ -20,6 +20,8 @@ Sources:
     of those files whose Huffman encoding (by the oracle) occurs, behind a
     matching H-bit/length prefix octet, inside a hex vector of the same file.
     The reference's expected bytes therefore pin these pairs.
+  * frame_test.go:16-50, 62-77   -> varint_vectors.json (HTTP/3 draft varints:
+    shortest and longer encodings, the write overflow, the frame header read)
   * hc/statictable.go            -> static_tables.json (HPACK 1-61, QPACK 0-98 entries)
   * hc/testcases_test.go:46-435  -> header_cases.json (header lists with their
     HPACK block, QPACK encoder-stream updates and header block, and the
@@ -114,6 +116,32 @@ def int_vectors():
             bad.append({"hex": m.group(1), "prefix": 8, "src": f"hc/io_test.go:{i + 1}"})
     assert len(ok) == 9 and len(bad) == 2, (len(ok), len(bad))
     return {"ints": ok, "overflow": bad}
+
+
+def varint_vectors():
+    lines = _read("frame_test.go")
+    out = {"shortest": [], "longer": [], "src": "frame_test.go"}
+    cur = None
+    for i, ln in enumerate(lines):
+        if "var varints = " in ln:
+            cur = out["shortest"]
+        elif "var longerVarints = " in ln:
+            cur = out["longer"]
+        m = re.match(r"^\s*\{(.+?),\s*\[\]byte\{([^}]*)\}\},", ln)
+        if m and cur is not None:
+            expr = m.group(1).strip().replace(" ", "")
+            if expr.startswith("1<<") and expr.endswith("-1"):
+                v = (1 << int(expr[3:-2])) - 1
+            elif expr.startswith("1<<"):
+                v = 1 << int(expr[3:])
+            else:
+                v = int(expr)
+            b = bytes(int(x, 0) for x in m.group(2).replace(" ", "").split(","))
+            cur.append({"value": str(v), "hex": b.hex(), "src": f"frame_test.go:{i + 1}"})
+    assert len(out["shortest"]) == 9 and len(out["longer"]) == 7, (len(out["shortest"]), len(out["longer"]))
+    out["too_large"] = {"value": str(1 << 63), "src": "frame_test.go:62-67"}
+    out["frame"] = {"hex": "010700", "type": 7, "payload": "00", "src": "frame_test.go:69-80"}
+    return out
 
 
 def static_tables():
@@ -294,6 +322,7 @@ def main():
         "string_vectors.json": string_vectors(),
         "bitio_vectors.json": bitio_vectors(),
         "int_vectors.json": int_vectors(),
+        "varint_vectors.json": varint_vectors(),
         "static_tables.json": static_tables(),
         "header_cases.json": header_cases(),
         "embedded_literals.json": embedded_literals(),

@@ -6,6 +6,7 @@
     decoded output; the parse, scans, gather, decode and finish kernels all
     inside the timed region;
   * read_ints_dev: batch Reader.ReadInt, integers/s;
+  * read_varints_dev: batch frameReader.ReadVarint, varints/s;
   * HPACK batch header-block decode (minhq_amd.headers): host walk, GPU
     string batch and table replay timed separately, beside the same blocks
     through the CPU oracle's ReadString (one core).
@@ -94,6 +95,24 @@ def main():
     ms = timed(lambda: codec.read_ints_dev(t_iblk, t_ipos, t_ilim, t_ipf, t_val, t_inx, t_ist), 20)
     assert np.array_equal(t_val.cpu().numpy().view(np.uint64), vals)
     res["read_ints_dev"] = {"ints": len(ints), "ms": round(ms, 4), "gints_s": round(len(ints) / (ms * 1e-3) / 1e9, 2)}
+
+    # HTTP/3 (draft) varints of every length class
+    vv = rng.integers(0, 1 << 62, size=args.literals, dtype=np.uint64) >> rng.integers(
+        0, 62, size=args.literals).astype(np.uint64)
+    encs, _ = codec.write_varints([int(v) for v in vv])
+    vblk = np.frombuffer(b"".join(encs), dtype=np.uint8)
+    vpos = np.zeros(len(encs), dtype=np.uint64)
+    vpos[1:] = np.cumsum([len(x) for x in encs])[:-1]
+    t_vblk = torch.from_numpy(vblk.copy()).to(dev)
+    t_vpos = torch.from_numpy(vpos.view(np.int64)).to(dev)
+    t_vlim = torch.full((len(encs),), len(vblk), dtype=torch.int64, device=dev)
+    t_vval = torch.empty(len(encs), dtype=torch.int64, device=dev)
+    t_vnx = torch.empty(len(encs), dtype=torch.int64, device=dev)
+    t_vst = torch.empty(len(encs), dtype=torch.uint8, device=dev)
+    ms = timed(lambda: codec.read_varints_dev(t_vblk, t_vpos, t_vlim, t_vval, t_vnx, t_vst), 20)
+    assert np.array_equal(t_vval.cpu().numpy().view(np.uint64), vv)
+    res["read_varints_dev"] = {"varints": len(encs), "ms": round(ms, 4),
+                               "gvarints_s": round(len(encs) / (ms * 1e-3) / 1e9, 2)}
 
     # HPACK blocks of literals (Huffman by Auto) from the netbsd.qif header set
     with open(os.path.join(REPO, "tests", "golden", "netbsd_qif.json")) as f:
