@@ -211,7 +211,8 @@ struct BitBuf {
 // The EOS prefix (INVALID when a 31st bit follows) and a long code running
 // past the end both finish the literal: `lim` = -1 ends the fast loop and
 // `bad` carries the status.
-__device__ __forceinline__ void fast_step(const Smem &sm, WaveSmem &ws, BitBuf &in, OutAcc &out, uint32_t endbit,
+template <class Acc>
+__device__ __forceinline__ void fast_step(const Smem &sm, uint32_t *otgt, BitBuf &in, Acc &out, uint32_t endbit,
                                           int &lim, uint32_t &bad) {
 #ifdef MHQ_X_NOLUT  // timing experiment only (wrong output): every probe is a 2-symbol 10-bit entry
   uint32_t e = lut1_entry(97, 97, 10, 2) ^ (in.top32() & 0x07070000u);
@@ -240,7 +241,7 @@ __device__ __forceinline__ void fast_step(const Smem &sm, WaveSmem &ws, BitBuf &
   out.put(e >> 16, (e >> 8) & 0xffu);
   in.consume(e);
   in.refill();
-  out.flush(ws.out_w);
+  out.flush(otgt);
 }
 
 // The last (< 24) bits of a literal whose output region is not truncating:
@@ -515,7 +516,7 @@ __device__ __forceinline__ void decode_piece(const Smem &sm, WaveSmem &ws, uint3
         }
       }
 #endif
-      fast_step(sm, ws, in, out, endbit, lim, bad);
+      fast_step(sm, ws.out_w, in, out, endbit, lim, bad);
       if ((int)in.p > lim) {  // this literal's fast part is over (lim = -1: the literal is finished)
         atomicOr(&ws.out_w[out.ow], (uint32_t)out.acc);  // bits of a completed word not yet written
         const uint32_t st = lim < 0 ? 1u | (bad << 1) : 0u;
@@ -553,6 +554,183 @@ __device__ __forceinline__ void decode_piece(const Smem &sm, WaveSmem &ws, uint3
                               : decode_checked(sm, ws, B.p, B.endbit, B.optr, B.oend);
   }
   wave_sync();
+}
+
+// ---- oversized tiles: literals streamed through per-lane windows ----------
+// A tile whose bytes exceed the slices (long literals: config 4's Zipf tail,
+// config 5's 438-byte literals) is decoded with every lane on a literal of its
+// own (lane l: literals l, l + 64), in wave-wide rounds.  Each round a lane
+// stages the next 128 B of its literal (from the 16-B chunk holding its bit
+// position) into a private LDS window — the windows reuse the wave's input
+// and output slices — and runs the fast steps until its window runs low or
+// its literal ends; the end runs the checked loop (the reference's end and
+// INVALID rules).  Output goes straight to global memory from the register
+// accumulator (OutAccG), which lives across rounds.  Literals whose output
+// region truncates are decoded by their lane with decode_literal_global.
+
+constexpr uint32_t kLongWords = 32;  // a lane's window: 128 B, 8 aligned 16-B chunks
+static_assert(sizeof(uint32_t) * kLongWords * kWave <= sizeof(uint32_t) * (kWIn / 4 + 4 + kWOut / 4 + 4),
+              "the lanes' windows fit the wave's slices");
+
+// Output bytes in registers, stored straight to global memory: `acc` holds
+// the bytes from word ow of the literal's 4-B aligned output base up, `ab`
+// bits of it decided.  A completed word inside the literal's region leaves as
+// a dword store; the first word of a region that starts mid-word is shared
+// with the previous literal's region, so it is kept in `first` and finish()
+// writes its bytes one by one, as it does the decided bytes of the last word.
+struct OutAccG {
+  uint64_t acc;
+  uint32_t ow, ab, owf, first, rs;
+  __device__ __forceinline__ void init(uint32_t optr) {
+    acc = 0;
+    ow = optr >> 2;
+    ab = (optr & 3u) * 8u;
+    owf = (optr + 3u) >> 2;  // the first word owned whole
+    first = 0;
+    rs = optr;
+  }
+  __device__ __forceinline__ void put(uint32_t syms, uint32_t nbits) {
+    acc |= (uint64_t)syms << ab;
+    ab += nbits;
+  }
+  __device__ __forceinline__ void flush(uint32_t *gout) {
+    const bool full = ab >= 32u;
+    if (full && ow >= owf) gout[ow] = (uint32_t)acc;
+    first = (full && ow < owf) ? (uint32_t)acc : first;
+    acc >>= ab & 32u;
+    ow += ab >> 5;
+    ab &= 31u;
+  }
+  __device__ __forceinline__ void finish(uint32_t *gout) {
+    flush(gout);
+    uint8_t *g8 = (uint8_t *)gout;
+    const uint32_t hi = ab >> 3, lo = ow < owf ? (rs & 3u) : 0u;
+    if (ow >= owf && (rs & 3u)) {
+      for (uint32_t x = rs & 3u; x < 4u; x++) g8[(owf - 1u) * 4u + x] = (uint8_t)(first >> (8u * x));
+    }
+    for (uint32_t x = lo; x < hi; x++) g8[ow * 4u + x] = (uint8_t)(acc >> (8u * x));
+  }
+  __device__ __forceinline__ uint32_t optr() const { return ow * 4u + (ab >> 3); }
+};
+
+// The checked loop of decode_checked on a window, with the lane's running
+// accumulator (roomy literals only: no buffer-full rule).  Returns the status.
+__device__ __forceinline__ uint32_t end_checked_g(const Smem &sm, const uint32_t *win, uint32_t p, uint32_t endbit,
+                                                  OutAccG &out, uint32_t *gout) {
+  BitBuf in;
+  in.init(win, p);
+  uint32_t bad = 0;
+  bool fin = false;
+  while (!fin) {
+    in.refill();
+    const uint32_t w = in.top32();
+    const uint32_t left = endbit - in.p;
+    const uint32_t e = sm.lut1[w >> (32 - kLut1Bits)];
+    uint32_t tot = e & 0xffu, ns8 = (e >> 8) & 0xffu, syms = e >> 16, len0 = sm.clen[(e >> 16) & 0xffu];
+    if (e == 0) {
+      const uint32_t L = long_code(sm.lut2, w, syms);
+      len0 = tot = L ? L : 0xffffffffu;
+      ns8 = 8u;
+      bad |= L == 0 && left > (uint32_t)kEosOnes;
+    }
+    const uint32_t c8 = tot <= left ? ns8 : (len0 <= left ? 8u : 0u);
+    const uint32_t cons = c8 == 16u ? tot : (c8 ? len0 : 0u);
+    out.put(__builtin_amdgcn_ubfe(syms, 0, c8), c8);
+    in.bb <<= cons & 63u;
+    in.p += cons;
+    fin = c8 == 0;
+    out.flush(gout);
+  }
+  return bad;
+}
+
+__device__ void decode_tile_long(const Smem &sm, WaveSmem &ws, const uint8_t *__restrict__ in,
+                                 const uint64_t *__restrict__ in_off, uint64_t in_bias, uint8_t *__restrict__ out,
+                                 const uint64_t *__restrict__ out_off, uint64_t out_bias,
+                                 uint32_t *__restrict__ out_len, uint8_t *__restrict__ status, uint64_t s,
+                                 uint32_t cnt, uint32_t lane) {
+  uint32_t *win = ws.in_w + lane * kLongWords;  // spans the input and output slices
+  constexpr uint32_t kWinBits = kLongWords * 32u;
+  constexpr uint32_t kSafe = kWinBits - 96u;  // fast steps stay below: 24 bits + two words of look-ahead
+  uint32_t j = lane;
+  bool have = false;
+  uint64_t ib = 0, ie = 0, ob = 0;
+  uint64_t rel = 0;  // bits of the literal consumed
+  uint32_t *gout = nullptr;
+  OutAccG acc;
+  acc.init(0);
+  uint32_t ostart = 0;
+  // next literal of this lane (roomy ones stay; the rest are done at once from global memory)
+  auto next_lit = [&]() {
+    have = false;
+    while (j < cnt) {
+      ib = in_off[s + j];
+      ie = in_off[s + j + 1];
+      ob = out_off[s + j];
+      const uint64_t oe = out_off[s + j + 1];
+      uint8_t *o = out + (ob - out_bias);
+      if (ie == ib) {  // nothing to read: Read at EOF
+        out_len[s + j] = 0;
+        status[s + j] = 0;
+      } else if (oe - ob < (ie - ib) * 8u / 5u) {  // a truncating region: the exact slow path
+        decode_literal_global(in + (ib - in_bias), ie - ib, o, oe - ob, sm, out_len + s + j, status + s + j);
+      } else {
+        gout = (uint32_t *)((uintptr_t)o & ~(uintptr_t)3);
+        ostart = (uint32_t)((uintptr_t)o & 3u);
+        acc.init(ostart);
+        rel = 0;
+        have = true;
+        return;
+      }
+      j += kWave;
+    }
+  };
+  next_lit();
+  while (__ballot(have)) {
+    // stage: the 8 aligned chunks from the one holding the lane's bit position
+    uint32_t p = 0, endw = 0;
+    if (have) {
+      const uint8_t *a = in + (ib - in_bias) + (rel >> 3);
+      const uint32_t delta = (uint32_t)((uintptr_t)a & 15u);
+      const u32x4 *src = (const u32x4 *)(a - delta);
+      const uint8_t *last = in + (ie - in_bias) - 1;  // the literal's last byte
+      const uint32_t lastc = (uint32_t)(((uintptr_t)last - (uintptr_t)src) >> 4);
+#pragma unroll
+      for (int k = 0; k < (int)(kLongWords / 4); k++) {
+        u32x4 v = __builtin_nontemporal_load(src + min((uint32_t)k, lastc));  // holds a valid byte
+        v.x = __builtin_bswap32(v.x);
+        v.y = __builtin_bswap32(v.y);
+        v.z = __builtin_bswap32(v.z);
+        v.w = __builtin_bswap32(v.w);
+        *(u32x4 *)(win + 4u * k) = v;
+      }
+      p = delta * 8u + (uint32_t)(rel & 7u);
+      endw = p + (uint32_t)((ie - ib) * 8u - rel);  // the literal's end in window bits (may lie beyond)
+    }
+    wave_sync();
+    if (have) {
+      const bool ends_here = endw + 64u <= kWinBits;
+      BitBuf bin;
+      bin.init(win, p);
+      uint32_t bad = 0;
+      const int lim0 = ends_here ? (int)endw - 24 : (int)kSafe;
+      int lim = lim0;
+      while ((int)bin.p <= lim) fast_step(sm, gout, bin, acc, endw, lim, bad);
+      const bool stopped = lim == -1 && lim0 != -1;  // a fast step finished the literal (EOS prefix, long code past the end)
+      if (stopped || ends_here) {
+        const uint32_t st = stopped ? bad : end_checked_g(sm, win, bin.p, endw, acc, gout);
+        const uint32_t got = acc.optr() - ostart;
+        acc.finish(gout);
+        out_len[s + j] = got;
+        status[s + j] = (uint8_t)st;
+        j += kWave;
+        next_lit();
+      } else {
+        rel += bin.p - p;
+      }
+    }
+    wave_sync();  // every lane is done reading its window (look-ahead reads reach the neighbour's)
+  }
 }
 
 // Slow path: a tile whose bytes exceed the slices, in greedy pieces staged
@@ -691,7 +869,16 @@ __global__ __launch_bounds__(kT) void decode_kernel(const uint8_t *__restrict__ 
       pd_s = s;
       pd_m = cnt;
     } else {
-      decode_tile_pieces(sm, ws, in, in_off, in_bias, out, out_off, out_bias, out_len, status, s, cnt, lane);
+      // a tile a little over the slice (short literals with a few long ones)
+      // goes in staged pieces; one of long literals streams through windows
+#ifdef MHQ_X_NOLONG  // timing experiment: the piece path for every oversized tile
+      if (true)
+#else
+      if ((ie - ib) <= 2u * (uint64_t)kWIn && (oe - ob) <= 2u * (uint64_t)kWOut)
+#endif
+        decode_tile_pieces(sm, ws, in, in_off, in_bias, out, out_off, out_bias, out_len, status, s, cnt, lane);
+      else
+        decode_tile_long(sm, ws, in, in_off, in_bias, out, out_off, out_bias, out_len, status, s, cnt, lane);
     }
     TL(3 + 3 * tl_j);
     tl_j++;
