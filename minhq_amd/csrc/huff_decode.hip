@@ -83,6 +83,7 @@ struct Smem {
   uint16_t lut2[kLut2Size];
   uint8_t clen[256];  // code length per symbol (len0 of a LUT1 entry, for the checked loop)
   uint32_t next_tile;
+  uint32_t tl;  // the tile length this launch uses (see decode_kernel)
   WaveSmem w[kWaves];
 };
 
@@ -792,7 +793,7 @@ __global__ __launch_bounds__(kT) void decode_kernel(const uint8_t *__restrict__ 
                                                     const uint32_t *__restrict__ g_lut1,
                                                     const uint16_t *__restrict__ g_lut2,
                                                     const uint8_t *__restrict__ g_len, uint64_t per_block,
-                                                    uint32_t tl) {
+                                                    uint32_t tl0) {
   __shared__ Smem sm;
   const uint32_t tid = threadIdx.x;
   const uint32_t lane = tid % kWave;
@@ -800,7 +801,6 @@ __global__ __launch_bounds__(kT) void decode_kernel(const uint8_t *__restrict__ 
   const uint64_t L0 = (uint64_t)blockIdx.x * per_block;
   if (L0 >= n) return;
   const uint64_t L1 = min(L0 + per_block, n);
-  const uint32_t ntiles = (uint32_t)((L1 - L0 + tl - 1) / tl);
   WaveSmem &ws = sm.w[wave];
   TL(0);
 
@@ -809,15 +809,35 @@ __global__ __launch_bounds__(kT) void decode_kernel(const uint8_t *__restrict__ 
   // tiles ahead of the one it decodes.
   uint32_t tile = wave, tile2 = tile + kWaves, tile3 = tile + 2 * kWaves;
   TileOff off, off2;
-  load_off(off, in_off, out_off, L0 + (uint64_t)tile * tl, L1, tl, lane);
-  load_off(off2, in_off, out_off, L0 + (uint64_t)tile2 * tl, L1, tl, lane);
+  load_off(off, in_off, out_off, L0 + (uint64_t)tile * tl0, L1, tl0, lane);
+  load_off(off2, in_off, out_off, L0 + (uint64_t)tile2 * tl0, L1, tl0, lane);
   for (uint32_t i = tid; i < kLut1Size / 4; i += kT) ((u32x4 *)sm.lut1)[i] = ((const u32x4 *)g_lut1)[i];
   for (uint32_t i = tid; i < kLut2Size / 8; i += kT) ((u32x4 *)sm.lut2)[i] = ((const u32x4 *)g_lut2)[i];
   if (tid < 64) ((uint32_t *)sm.clen)[tid] = ((const uint32_t *)g_len)[tid];
   if (tid == 0) sm.next_tile = 3 * kWaves;
   TileIn tin;
   load_in(tin, in, in_bias, uniform64(off.i0), uniform64(off.ie), lane);
+  // The tile length: the host's tl0 (every wave the same number of tiles)
+  // unless the batch's mean literal is too long for tl0 of them to fit the
+  // slices, with a 25 % margin; then the most that fit, if that still gives
+  // every lane a literal (longer literals keep tl0 and stream).  The boundary
+  // offsets load beside the tables.
+  if (tid == 0) {
+    const uint64_t nin = in_off[n] - in_off[0], nout = out_off[n] - out_off[0];
+    const uint64_t ain = (nin + n - 1) / n, aout = (nout + n - 1) / n;
+    const uint64_t fit_in = (uint64_t)(kWIn - 16) * 4u / (5u * ain + 8u);
+    const uint64_t fit_out = (uint64_t)(kWOut - 16) * 4u / (5u * aout + 8u);
+    const uint64_t fit = min(fit_in, fit_out);
+    sm.tl = fit >= (uint64_t)kWave && fit < (uint64_t)tl0 ? (uint32_t)fit : tl0;
+  }
   __syncthreads();
+  const uint32_t tl = __builtin_amdgcn_readfirstlane(sm.tl);
+  if (tl != tl0) {  // the loads above used tl0: again with tl
+    load_off(off, in_off, out_off, L0 + (uint64_t)tile * tl, L1, tl, lane);
+    load_off(off2, in_off, out_off, L0 + (uint64_t)tile2 * tl, L1, tl, lane);
+    load_in(tin, in, in_bias, uniform64(off.i0), uniform64(off.ie), lane);
+  }
+  const uint32_t ntiles = (uint32_t)((L1 - L0 + tl - 1) / tl);
   uint64_t pd_s = 0;  // the previous tile, still in the output slice: literals, output range
   uint32_t pd_m = 0, pd_lo = 0, pd_hi = 0;
   uint8_t *pd_o = nullptr;
