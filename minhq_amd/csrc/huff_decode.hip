@@ -563,8 +563,8 @@ __device__ __forceinline__ void decode_piece(const Smem &sm, WaveSmem &ws, uint3
 // own (lane l: literals l, l + 64), in wave-wide rounds.  Each round a lane
 // stages the next 128 B of its literal (from the 16-B chunk holding its bit
 // position) into a private LDS window — the windows reuse the wave's input
-// and output slices — and runs the fast steps until its window runs low or
-// its literal ends; the end runs the checked loop (the reference's end and
+// and output slices — and runs probes (long_step) until its window runs low
+// or its literal ends; the end runs the checked loop (the reference's end and
 // INVALID rules).  Output goes straight to global memory from the register
 // accumulator (OutAccG), which lives across rounds.  Literals whose output
 // region truncates are decoded by their lane with decode_literal_global.
@@ -645,6 +645,31 @@ __device__ __forceinline__ uint32_t end_checked_g(const Smem &sm, const uint32_t
   return bad;
 }
 
+// One probe of the stream path: a long code (or the EOS prefix) found by the
+// probe is resolved at once through LUT2 — long literals are where long
+// codes pile up (config 5 has nothing else), and the fast step would spend a
+// second LUT1 probe finding it again.  Same end rules as fast_step.
+template <class Acc>
+__device__ __forceinline__ void long_step(const Smem &sm, uint32_t *otgt, BitBuf &in, Acc &out, uint32_t endbit,
+                                          int &lim, uint32_t &bad) {
+  uint32_t e = sm.lut1[in.top32() >> (32 - kLut1Bits)];
+  if (e == 0) {
+    uint32_t sym = 0;
+    const uint32_t L = long_code(sm.lut2, in.top32(), sym);
+    const uint32_t left = endbit - in.p;
+    if (L == 0 || L > left) {
+      bad = L == 0 && left > (uint32_t)kEosOnes;  // a 31st bit exists: nil child (hc/huffman.go:111-113)
+      lim = -1;
+    } else {
+      e = L | (8u << 8) | (sym << 16);
+    }
+  }
+  out.put(e >> 16, (e >> 8) & 0xffu);
+  in.consume(e);
+  in.refill();
+  out.flush(otgt);
+}
+
 __device__ void decode_tile_long(const Smem &sm, WaveSmem &ws, const uint8_t *__restrict__ in,
                                  const uint64_t *__restrict__ in_off, uint64_t in_bias, uint8_t *__restrict__ out,
                                  const uint64_t *__restrict__ out_off, uint64_t out_bias,
@@ -716,7 +741,7 @@ __device__ void decode_tile_long(const Smem &sm, WaveSmem &ws, const uint8_t *__
       uint32_t bad = 0;
       const int lim0 = ends_here ? (int)endw - 24 : (int)kSafe;
       int lim = lim0;
-      while ((int)bin.p <= lim) fast_step(sm, gout, bin, acc, endw, lim, bad);
+      while ((int)bin.p <= lim) long_step(sm, gout, bin, acc, endw, lim, bad);
       const bool stopped = lim == -1 && lim0 != -1;  // a fast step finished the literal (EOS prefix, long code past the end)
       if (stopped || ends_here) {
         const uint32_t st = stopped ? bad : end_checked_g(sm, win, bin.p, endw, acc, gout);
