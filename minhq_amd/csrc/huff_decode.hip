@@ -569,7 +569,10 @@ __device__ __forceinline__ void decode_piece(const Smem &sm, WaveSmem &ws, uint3
 // accumulator (OutAccG), which lives across rounds.  Literals whose output
 // region truncates are decoded by their lane with decode_literal_global.
 
-constexpr uint32_t kLongWords = 32;  // a lane's window: 128 B, 8 aligned 16-B chunks
+#ifndef MHQ_DEC_LONGW  // a lane's window in words (multiple of 4)
+#define MHQ_DEC_LONGW 32
+#endif
+constexpr uint32_t kLongWords = MHQ_DEC_LONGW;  // a lane's window: 128 B, 8 aligned 16-B chunks
 static_assert(sizeof(uint32_t) * kLongWords * kWave <= sizeof(uint32_t) * (kWIn / 4 + 4 + kWOut / 4 + 4),
               "the lanes' windows fit the wave's slices");
 

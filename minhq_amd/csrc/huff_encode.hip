@@ -289,7 +289,11 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu((kT / 64 * M
       __syncthreads();
       if (tid < m) sm.order[sm.hist[bk] + rk] = (uint16_t)tid;
       __syncthreads();
+#ifdef MHQ_X_ENC_NOWORK  // timing experiment only (wrong output): staging, sort and stores, no encoding
+      if (false) {
+#else
       if (tid < m) {
+#endif
         const uint32_t lit = sm.order[tid];
         const uint32_t r0 = sm.rec[lit], r1 = sm.rec[lit + 1];
         const uint32_t bits = encode_one<kEmit>(sm, r0 & 0xffffu, r1 & 0xffffu, r0 >> 16);

@@ -1,10 +1,14 @@
 // mhq_api.cpp -- the C ABI of libmhq_huff.so (include/mhq_huff.h).
 //
 // Host-memory entry points shard the batch across the context's devices by
-// encoded bytes (literals are independent, no collective), run
-// H2D -> kernel -> D2H per shard on one host thread per device, and rebase the
-// offsets with a per-shard bias instead of rewriting them.  Device-resident
-// entry points only enqueue kernels on the caller's stream.
+// encoded bytes (literals are independent, no collective), one
+// host thread per device.  A device's shard runs as a pipeline of chunks of
+// about kChunkBytes on kPipe streams, each with its own staging buffers:
+// chunk c's H2D copies, kernel and D2H copies go on stream c % kPipe, so one
+// chunk's upload, another's kernel and a third's download overlap (stream
+// order keeps a staging set from being reused before its chunk is done).
+// Offsets are rebased with a per-chunk bias instead of being rewritten.
+// Device-resident entry points only enqueue kernels on the caller's stream.
 #include <hip/hip_runtime.h>
 #include <string.h>
 
@@ -50,13 +54,21 @@ struct Buffer {
   }
 };
 
+constexpr int kPipe = 3;                     // streams (and staging sets) per device for host-memory calls
+constexpr uint64_t kChunkBytes = 8ull << 20;  // input bytes per pipelined chunk
+
+struct Stage {
+  hipStream_t s = nullptr;
+  Buffer in, in_off, out, out_off, lens, status;
+};
+
 struct Device {
   int ordinal = 0;
   void *table_mem = nullptr;
   DevTables tables{};
   std::mutex mu;  // serialises host-memory calls (they share the staging buffers)
   hipStream_t stream = nullptr;
-  Buffer in, in_off, out, out_off, lens, status;
+  Stage st[kPipe];
 };
 
 }  // namespace
@@ -101,17 +113,21 @@ int init_device(Device *d, int ordinal) {
   d->tables.lut2 = (const uint16_t *)p_lut2;
   d->tables.len = (const uint8_t *)p_len;
   MHQ_TRY(hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking));
+  for (Stage &x : d->st) MHQ_TRY(hipStreamCreateWithFlags(&x.s, hipStreamNonBlocking));
   return MHQ_OK;
 }
 
 void free_device(Device *d) {
   (void)hipSetDevice(d->ordinal);
-  d->in.release();
-  d->in_off.release();
-  d->out.release();
-  d->out_off.release();
-  d->lens.release();
-  d->status.release();
+  for (Stage &x : d->st) {
+    x.in.release();
+    x.in_off.release();
+    x.out.release();
+    x.out_off.release();
+    x.lens.release();
+    x.status.release();
+    if (x.s) (void)hipStreamDestroy(x.s);
+  }
   if (d->stream) (void)hipStreamDestroy(d->stream);
   if (d->table_mem) (void)hipFree(d->table_mem);
 }
@@ -146,48 +162,77 @@ struct HostJob {
   uint8_t *status;
 };
 
-// Runs literals [a, b) of a host-memory job on one device.
+// Enqueues literals [a, b) of a host-memory job on one stage's stream.
+int run_chunk(Device *d, Stage &S, const HostJob &j, uint64_t a, uint64_t b) {
+  const uint64_t m = b - a;
+  if (m == 0) return MHQ_OK;
+  hipStream_t s = S.s;
+  const uint64_t in_bias = j.in_off[a];
+  const uint64_t in_bytes = j.in_off[b] - j.in_off[a];
+  MHQ_TRY(hipMemcpyAsync(S.in.p, j.in + (j.in_off[a] - j.in_off[0]), in_bytes, hipMemcpyHostToDevice, s));
+  MHQ_TRY(hipMemcpyAsync(S.in_off.p, j.in_off + a, (m + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, s));
+  const uint8_t *din = (const uint8_t *)S.in.p;
+  const uint64_t *din_off = (const uint64_t *)S.in_off.p;
+  if (j.op == Op::kEncodeLen) {
+    MHQ_TRY(mhq::launch_encode_len(d->tables, din, din_off, in_bias, m, (uint32_t *)S.lens.p, s));
+    return hip_rc(hipMemcpyAsync(j.lens + a, S.lens.p, m * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+  }
+  const uint64_t out_bias = j.out_off[a];
+  const uint64_t out_bytes = j.out_off[b] - j.out_off[a];
+  MHQ_TRY(hipMemcpyAsync(S.out_off.p, j.out_off + a, (m + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, s));
+  // Regions are fully defined on return: unspecified bytes come back as zeros.
+  MHQ_TRY(hipMemsetAsync(S.out.p, 0, out_bytes, s));
+  uint8_t *dout = (uint8_t *)S.out.p;
+  const uint64_t *dout_off = (const uint64_t *)S.out_off.p;
+  if (j.op == Op::kEncode) {
+    MHQ_TRY(mhq::launch_encode(d->tables, din, din_off, in_bias, m, dout, dout_off, out_bias, s));
+  } else {
+    MHQ_TRY(mhq::launch_decode(d->tables, din, din_off, in_bias, m, dout, dout_off, out_bias,
+                               (uint32_t *)S.lens.p, (uint8_t *)S.status.p, s));
+    MHQ_TRY(hipMemcpyAsync(j.lens + a, S.lens.p, m * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    MHQ_TRY(hipMemcpyAsync(j.status + a, S.status.p, m, hipMemcpyDeviceToHost, s));
+  }
+  return hip_rc(
+      hipMemcpyAsync(j.out + (j.out_off[a] - j.out_off[0]), dout, out_bytes, hipMemcpyDeviceToHost, s));
+}
+
+// Runs literals [a, b) of a host-memory job on one device: chunks of about
+// kChunkBytes of input, pipelined over the device's kPipe stages.
 int run_shard(Device *d, const HostJob &j, uint64_t a, uint64_t b) {
   const uint64_t m = b - a;
   if (m == 0) return MHQ_OK;
   std::lock_guard<std::mutex> lock(d->mu);
   MHQ_TRY(hipSetDevice(d->ordinal));
-  hipStream_t s = d->stream;
-  const uint64_t in_bias = j.in_off[a];
   const uint64_t in_bytes = j.in_off[b] - j.in_off[a];
-  MHQ_TRY(d->in.reserve(in_bytes + 16));
-  MHQ_TRY(d->in_off.reserve((m + 1) * sizeof(uint64_t)));
-  MHQ_TRY(hipMemcpyAsync(d->in.p, j.in + (j.in_off[a] - j.in_off[0]), in_bytes, hipMemcpyHostToDevice, s));
-  MHQ_TRY(hipMemcpyAsync(d->in_off.p, j.in_off + a, (m + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, s));
-  const uint8_t *din = (const uint8_t *)d->in.p;
-  const uint64_t *din_off = (const uint64_t *)d->in_off.p;
-  if (j.op == Op::kEncodeLen) {
-    MHQ_TRY(d->lens.reserve(m * sizeof(uint32_t)));
-    MHQ_TRY(mhq::launch_encode_len(d->tables, din, din_off, in_bias, m, (uint32_t *)d->lens.p, s));
-    MHQ_TRY(hipMemcpyAsync(j.lens + a, d->lens.p, m * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
-    return hip_rc(hipStreamSynchronize(s));
+  const size_t nch = (size_t)std::max<uint64_t>(1, std::min<uint64_t>(m, (in_bytes + kChunkBytes - 1) / kChunkBytes));
+  std::vector<uint64_t> cb = shard_bounds(j.in_off + a, m, nch);
+  // staging sized for the largest chunk, before anything is enqueued
+  uint64_t max_m = 0, max_in = 0, max_out = 0;
+  for (size_t c = 0; c < nch; c++) {
+    const uint64_t x = a + cb[c], y = a + cb[c + 1];
+    max_m = std::max(max_m, y - x);
+    max_in = std::max(max_in, j.in_off[y] - j.in_off[x]);
+    if (j.op != Op::kEncodeLen) max_out = std::max(max_out, j.out_off[y] - j.out_off[x]);
   }
-  const uint64_t out_bias = j.out_off[a];
-  const uint64_t out_bytes = j.out_off[b] - j.out_off[a];
-  MHQ_TRY(d->out.reserve(out_bytes + 16));
-  MHQ_TRY(d->out_off.reserve((m + 1) * sizeof(uint64_t)));
-  MHQ_TRY(hipMemcpyAsync(d->out_off.p, j.out_off + a, (m + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, s));
-  // Regions are fully defined on return: unspecified bytes come back as zeros.
-  MHQ_TRY(hipMemsetAsync(d->out.p, 0, out_bytes, s));
-  uint8_t *dout = (uint8_t *)d->out.p;
-  const uint64_t *dout_off = (const uint64_t *)d->out_off.p;
-  if (j.op == Op::kEncode) {
-    MHQ_TRY(mhq::launch_encode(d->tables, din, din_off, in_bias, m, dout, dout_off, out_bias, s));
-  } else {
-    MHQ_TRY(d->lens.reserve(m * sizeof(uint32_t)));
-    MHQ_TRY(d->status.reserve(m));
-    MHQ_TRY(mhq::launch_decode(d->tables, din, din_off, in_bias, m, dout, dout_off, out_bias,
-                               (uint32_t *)d->lens.p, (uint8_t *)d->status.p, s));
-    MHQ_TRY(hipMemcpyAsync(j.lens + a, d->lens.p, m * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
-    MHQ_TRY(hipMemcpyAsync(j.status + a, d->status.p, m, hipMemcpyDeviceToHost, s));
+  const int used = (int)std::min<size_t>(nch, kPipe);
+  for (int k = 0; k < used; k++) {
+    Stage &S = d->st[k];
+    MHQ_TRY(S.in.reserve(max_in + 16));
+    MHQ_TRY(S.in_off.reserve((max_m + 1) * sizeof(uint64_t)));
+    MHQ_TRY(S.lens.reserve(max_m * sizeof(uint32_t)));
+    if (j.op != Op::kEncodeLen) {
+      MHQ_TRY(S.out.reserve(max_out + 16));
+      MHQ_TRY(S.out_off.reserve((max_m + 1) * sizeof(uint64_t)));
+      MHQ_TRY(S.status.reserve(max_m));
+    }
   }
-  MHQ_TRY(hipMemcpyAsync(j.out + (j.out_off[a] - j.out_off[0]), dout, out_bytes, hipMemcpyDeviceToHost, s));
-  return hip_rc(hipStreamSynchronize(s));
+  int rc = MHQ_OK;
+  for (size_t c = 0; c < nch && rc == MHQ_OK; c++) rc = run_chunk(d, d->st[c % kPipe], j, a + cb[c], a + cb[c + 1]);
+  for (int k = 0; k < used; k++) {
+    const int r = hip_rc(hipStreamSynchronize(d->st[k].s));
+    if (rc == MHQ_OK) rc = r;
+  }
+  return rc;
 }
 
 int run_host(mhq_ctx *ctx, const HostJob &j, uint64_t n) {

@@ -78,6 +78,12 @@ def _p(a: np.ndarray, t):
     return a.ctypes.data_as(C.POINTER(t))
 
 
+def _alloc(alloc, n: int, dtype) -> np.ndarray:
+    if alloc is None:
+        return np.zeros(n, dtype=dtype)
+    return alloc(n * np.dtype(dtype).itemsize)[: n * np.dtype(dtype).itemsize].view(dtype)
+
+
 def _nonempty(a: np.ndarray) -> np.ndarray:
     # ctypes needs a valid pointer even for zero-length buffers
     return a if a.size else np.zeros(1, dtype=a.dtype)
@@ -123,39 +129,45 @@ class Codec:
             pass
 
     # ---------------- host-memory batches ----------------
-    def encode_len(self, data: np.ndarray, off: np.ndarray) -> np.ndarray:
+    # `alloc(nbytes) -> uint8 array` supplies the output buffers of the
+    # host-memory calls (e.g. pinned memory for the PCIe-inclusive rate); the
+    # default is zeroed pageable numpy memory.
+    def encode_len(self, data: np.ndarray, off: np.ndarray, alloc=None) -> np.ndarray:
         n = len(off) - 1
-        out = np.zeros(max(n, 1), dtype=np.uint32)
+        out = _alloc(alloc, max(n, 1), np.uint32)
         data = _nonempty(np.ascontiguousarray(data, dtype=np.uint8))
         off = np.ascontiguousarray(off, dtype=np.uint64)
         check(self._L.mhq_huff_encode_len(self._h, _p(data, C.c_uint8), _p(off, C.c_uint64), n,
                                           _p(out, C.c_uint32)), "mhq_huff_encode_len")
         return out[:n]
 
-    def encode(self, data: np.ndarray, off: np.ndarray) -> Tuple[np.ndarray, np.ndarray]:
+    def encode(self, data: np.ndarray, off: np.ndarray, alloc=None) -> Tuple[np.ndarray, np.ndarray]:
         """Returns (encoded bytes, encoded offsets) for a packed batch."""
         n = len(off) - 1
+        # enc_len is read back by the host scan: pageable memory (pinned host
+        # memory can be slow to read from the CPU); the offsets are only written.
         enc_len = self.encode_len(data, off)
-        enc_off = np.zeros(n + 1, dtype=np.uint64)
+        enc_off = _alloc(alloc, n + 1, np.uint64)
+        enc_off[0] = 0
         if n:
             enc_off[1:] = np.cumsum(enc_len, dtype=np.uint64)
-        out = np.zeros(max(int(enc_off[-1]), 1), dtype=np.uint8)
+        out = _alloc(alloc, max(int(enc_off[-1]), 1), np.uint8)
         data = _nonempty(np.ascontiguousarray(data, dtype=np.uint8))
         off = np.ascontiguousarray(off, dtype=np.uint64)
         check(self._L.mhq_huff_encode(self._h, _p(data, C.c_uint8), _p(off, C.c_uint64), n,
                                       _p(out, C.c_uint8), _p(enc_off, C.c_uint64)), "mhq_huff_encode")
         return out[: int(enc_off[-1])], enc_off
 
-    def decode(self, enc: np.ndarray, off: np.ndarray, cap_off: Optional[np.ndarray] = None):
+    def decode(self, enc: np.ndarray, off: np.ndarray, cap_off: Optional[np.ndarray] = None, alloc=None):
         """Returns (out, cap_off, out_len, status) for a packed batch."""
         n = len(off) - 1
         off = np.ascontiguousarray(off, dtype=np.uint64)
         if cap_off is None:
             cap_off = capacity_offsets(off)
         cap_off = np.ascontiguousarray(cap_off, dtype=np.uint64)
-        out = np.zeros(max(int(cap_off[-1] - cap_off[0]) if n else 0, 1), dtype=np.uint8)
-        out_len = np.zeros(max(n, 1), dtype=np.uint32)
-        status = np.zeros(max(n, 1), dtype=np.uint8)
+        out = _alloc(alloc, max(int(cap_off[-1] - cap_off[0]) if n else 0, 1), np.uint8)
+        out_len = _alloc(alloc, max(n, 1), np.uint32)
+        status = _alloc(alloc, max(n, 1), np.uint8)
         enc = _nonempty(np.ascontiguousarray(enc, dtype=np.uint8))
         check(self._L.mhq_huff_decode(self._h, _p(enc, C.c_uint8), _p(off, C.c_uint64), n,
                                       _p(out, C.c_uint8), _p(cap_off, C.c_uint64), _p(out_len, C.c_uint32),
