@@ -107,8 +107,7 @@ def encoded_sizes(codec, batch, dev):
 
 
 def round_trip(codec, s, ev=None):
-    codec.encode_len_dev(s.data, s.off, s.enc_len)
-    codec.offsets_dev(s.enc_len, s.enc_off, s.cap_off)
+    codec.encode_layout_dev(s.data, s.off, s.enc_len, s.enc_off, s.cap_off)
     if ev is not None:
         ev[0].record()
     codec.encode_dev(s.data, s.off, s.enc, s.enc_off)

@@ -98,6 +98,14 @@ int mhq_huff_encode_len_dev(mhq_ctx *ctx, int dev, const uint8_t *in, const uint
  * encode output offsets and the matching decode capacities. */
 int mhq_huff_offsets_dev(mhq_ctx *ctx, int dev, const uint32_t *enc_len, uint64_t n, uint64_t base,
                          uint64_t *out_off, uint64_t *cap_off, void *stream);
+/* mhq_huff_encode_len_dev followed by mhq_huff_offsets_dev (cap_off may be
+ * NULL), with the scan's first pass folded into the sizing kernel: the whole
+ * output layout of an encode in two launches.  Replaces the sizing half of
+ * hc/io.go:157-172 (the temp-buffer encode that Auto mode measures) for a
+ * batch, plus the placement the caller would otherwise do on the host. */
+int mhq_huff_encode_layout_dev(mhq_ctx *ctx, int dev, const uint8_t *in, const uint64_t *in_off, uint64_t n,
+                               uint64_t base, uint32_t *enc_len, uint64_t *out_off, uint64_t *cap_off,
+                               void *stream);
 /* cap_off[i] = base + sum_{j<i} floor(8*(in_off[j+1]-in_off[j])/5). */
 int mhq_huff_capacity_dev(mhq_ctx *ctx, int dev, const uint64_t *in_off, uint64_t n, uint64_t base,
                           uint64_t *cap_off, void *stream);

@@ -51,6 +51,7 @@ SIGNATURES = {
     "mhq_huff_decode": (C.c_int, [vp, u8p, u64p, C.c_uint64, u8p, u64p, u32p, u8p]),
     "mhq_huff_encode_len_dev": (C.c_int, [vp, C.c_int, vp, vp, C.c_uint64, vp, vp]),
     "mhq_huff_offsets_dev": (C.c_int, [vp, C.c_int, vp, C.c_uint64, C.c_uint64, vp, vp, vp]),
+    "mhq_huff_encode_layout_dev": (C.c_int, [vp, C.c_int, vp, vp, C.c_uint64, C.c_uint64, vp, vp, vp, vp]),
     "mhq_huff_capacity_dev": (C.c_int, [vp, C.c_int, vp, C.c_uint64, C.c_uint64, vp, vp]),
     "mhq_huff_encode_dev": (C.c_int, [vp, C.c_int, vp, vp, C.c_uint64, vp, vp, vp]),
     "mhq_huff_decode_dev": (C.c_int, [vp, C.c_int, vp, vp, C.c_uint64, vp, vp, vp, vp, vp]),

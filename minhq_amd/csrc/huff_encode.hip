@@ -324,7 +324,7 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu((kT / 64 * M
 // so lanes that look up different bytes rarely share a bank.  Per byte: the shifted
 // byte as address, one LDS read, the chunk's in-range mask bit times the
 // length added in.
-constexpr int kLenT = 256;
+constexpr int kLenT = kLenSumBlock;
 constexpr int kPre = 5;  // chunks loaded ahead: literals of up to 64 bytes
 
 struct LenAhead {
@@ -379,26 +379,51 @@ __device__ __forceinline__ uint32_t len_sum(const LenAhead &t, const uint8_t *__
 __global__ __launch_bounds__(kLenT) void encode_len_kernel(const uint8_t *__restrict__ in,
                                                            const uint64_t *__restrict__ in_off, uint64_t in_bias,
                                                            uint64_t n, uint32_t *__restrict__ enc_len,
-                                                           const uint8_t *__restrict__ g_len) {
+                                                           const uint8_t *__restrict__ g_len,
+                                                           uint64_t *__restrict__ block_sums) {
   __shared__ uint32_t lens[256];
+  __shared__ uint64_t part[2 * (kLenT / kWave)];
   lens[threadIdx.x] = g_len[threadIdx.x];
   __syncthreads();
   const uint64_t i = (uint64_t)blockIdx.x * kLenT + threadIdx.x;
-  if (i >= n) return;
-  LenAhead t{};
-  t.a = in_off[i] - in_bias;
-  t.b = in_off[i + 1] - in_bias;
-  len_load_chunks(t, in);
-  enc_len[i] = (len_sum(t, in, lens) + 7u) >> 3;
+  uint32_t el = 0;
+  if (i < n) {
+    LenAhead t{};
+    t.a = in_off[i] - in_bias;
+    t.b = in_off[i + 1] - in_bias;
+    len_load_chunks(t, in);
+    el = (len_sum(t, in, lens) + 7u) >> 3;
+    enc_len[i] = el;
+  }
+  if (!block_sums) return;  // uniform over the grid
+  // the block's (sum of enc_len, sum of decode capacities) for the offsets scan
+  uint64_t sa = el, sb = ((uint64_t)el * 8u) / 5u;
+#pragma unroll
+  for (int d = 1; d < kWave; d <<= 1) {
+    sa += __shfl_xor(sa, d);
+    sb += __shfl_xor(sb, d);
+  }
+  const int lane = threadIdx.x % kWave, wave = threadIdx.x / kWave;
+  if (lane == 0) {
+    part[2 * wave] = sa;
+    part[2 * wave + 1] = sb;
+  }
+  __syncthreads();
+  if (threadIdx.x < 2) {
+    uint64_t v = 0;
+#pragma unroll
+    for (int w = 0; w < kLenT / kWave; w++) v += part[2 * w + threadIdx.x];
+    block_sums[2 * blockIdx.x + threadIdx.x] = v;
+  }
 }
 
 }  // namespace
 
 hipError_t launch_encode_len(const DevTables &t, const uint8_t *in, const uint64_t *in_off, uint64_t in_bias,
-                             uint64_t n, uint32_t *enc_len, hipStream_t s) {
+                             uint64_t n, uint32_t *enc_len, hipStream_t s, uint64_t *block_sums) {
   if (n == 0) return hipSuccess;
   encode_len_kernel<<<dim3((unsigned)((n + kLenT - 1) / kLenT)), dim3(kLenT), 0, s>>>(in, in_off, in_bias, n,
-                                                                                      enc_len, t.len);
+                                                                                      enc_len, t.len, block_sums);
   return hipGetLastError();
 }
 

@@ -18,8 +18,17 @@ struct DevTables {
 
 // All offsets arrays have n+1 entries; literal i occupies
 // base[off[i] - bias .. off[i+1] - bias).
+// encode_len's block: with `block_sums` not null, block k writes
+// (sum of enc_len, sum of floor(8*enc_len/5)) over literals
+// [k*kLenSumBlock, (k+1)*kLenSumBlock) to block_sums[2k], [2k+1]
+// (ceil(n/kLenSumBlock) pairs), the first pass of the offsets scan.
+constexpr int kLenSumBlock = 256;
 hipError_t launch_encode_len(const DevTables &t, const uint8_t *in, const uint64_t *in_off,
-                             uint64_t in_bias, uint64_t n, uint32_t *enc_len, hipStream_t s);
+                             uint64_t in_bias, uint64_t n, uint32_t *enc_len, hipStream_t s,
+                             uint64_t *block_sums = nullptr);
+// launch_offsets over encode_len's block sums (one pass instead of two).
+hipError_t launch_offsets_sums(const uint32_t *enc_len, uint64_t n, const uint64_t *block_sums, uint64_t base,
+                               uint64_t *out_off, uint64_t *cap_off, hipStream_t s);
 hipError_t launch_encode(const DevTables &t, const uint8_t *in, const uint64_t *in_off,
                          uint64_t in_bias, uint64_t n, uint8_t *out, const uint64_t *out_off,
                          uint64_t out_bias, hipStream_t s);

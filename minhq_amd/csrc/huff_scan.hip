@@ -132,21 +132,38 @@ __global__ __launch_bounds__(kScanBlock) void scan_reduce_kernel(F f, uint64_t n
 }
 
 template <class F>
-__global__ __launch_bounds__(kScanBlock) void scan_apply_kernel(F f, uint64_t n, const uint64_t *sums,
+// `sums` holds (a, b) pairs for consecutive groups of kChunk / g items: the
+// reduce pass writes one per chunk (g = 1), encode_len one per block of
+// kChunk / 8 literals (g = 8).
+__global__ __launch_bounds__(kScanBlock) void scan_apply_kernel(F f, uint64_t n, const uint64_t *sums, uint32_t g,
                                                                  uint64_t base, uint64_t *oa, uint64_t *ob) {
   __shared__ uint64_t sh[2 * kWaves];
   const int tid = threadIdx.x, lane = tid % kWave, wave = tid / kWave;
-  // prefix of the chunks before this one
-  uint64_t pa = 0, pb = 0;
-  for (uint32_t j = tid; j < blockIdx.x; j += kScanBlock) {
-    pa += sums[2 * j];
-    pb += sums[2 * j + 1];
-  }
-  block_sum2(pa, pb, sh);
-  // this chunk
+  // this chunk's items first: their loads are in flight during the prefix
   const uint64_t i0 = (uint64_t)blockIdx.x * kChunk + (uint64_t)tid * kItems;
   uint64_t a[kItems], b[kItems];
   f.load(i0, a, b);
+  // prefix of the chunks before this one
+  typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+  const u64x2 *sp = (const u64x2 *)sums;
+  // (batches of eight independent loads per thread: one L2 round trip per
+  // batch, not per pair)
+  uint64_t pa = 0, pb = 0;
+  const uint32_t cnt = blockIdx.x * g;
+  for (uint32_t j0 = 0; j0 < cnt; j0 += 8u * kScanBlock) {
+    u64x2 v[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      const uint32_t j = j0 + (uint32_t)k * kScanBlock + tid;
+      v[k] = j < cnt ? sp[j] : u64x2{0ull, 0ull};
+    }
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      pa += v[k].x;
+      pb += v[k].y;
+    }
+  }
+  block_sum2(pa, pb, sh);
   uint64_t ta = 0, tb = 0;
 #pragma unroll
   for (int k = 0; k < kItems; k++) {
@@ -172,8 +189,23 @@ __global__ __launch_bounds__(kScanBlock) void scan_apply_kernel(F f, uint64_t n,
     ra += a[k];
     rb += b[k];
   }
-  typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
-  if (i0 + kItems <= n + 1) {  // a whole run of outputs: 16-B stores (i0 is a multiple of 8)
+  const uint64_t c0 = (uint64_t)blockIdx.x * kChunk;
+  if (c0 + kChunk <= n + 1) {
+    // a whole chunk: through LDS, so each wave-wide 16-B store covers 1 KiB
+    // of consecutive offsets (stores straight from the owning threads touch
+    // 64 lines each)
+    __shared__ u64x2 st[kChunk];  // a's chunk in .x, b's in .y
+#pragma unroll
+    for (int k = 0; k < kItems; k++) st[tid * kItems + k] = u64x2{xa[k], xb[k]};
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kItems / 2; k++) {
+      const uint32_t j = 2u * ((uint32_t)tid + (uint32_t)k * kScanBlock);
+      const u64x2 v0 = st[j], v1 = st[j + 1];
+      if (oa) *(u64x2 *)(oa + c0 + j) = u64x2{v0.x, v1.x};
+      if (ob) *(u64x2 *)(ob + c0 + j) = u64x2{v0.y, v1.y};
+    }
+  } else if (i0 + kItems <= n + 1) {  // a whole run of outputs: 16-B stores (i0 is a multiple of 8)
 #pragma unroll
     for (int k = 0; k < kItems; k += 2) {
       if (oa) *(u64x2 *)(oa + i0 + k) = u64x2{xa[k], xa[k + 1]};
@@ -198,7 +230,7 @@ hipError_t run_scan(F f, uint64_t n, uint64_t base, uint64_t *oa, uint64_t *ob, 
   hipError_t e = hipMallocAsync((void **)&sums, nb * 2 * sizeof(uint64_t), s);
   if (e != hipSuccess) return e;
   scan_reduce_kernel<F><<<dim3((unsigned)nb), dim3(kScanBlock), 0, s>>>(f, n, sums);
-  scan_apply_kernel<F><<<dim3((unsigned)nb), dim3(kScanBlock), 0, s>>>(f, n, sums, base, oa, ob);
+  scan_apply_kernel<F><<<dim3((unsigned)nb), dim3(kScanBlock), 0, s>>>(f, n, sums, 1u, base, oa, ob);
   e = hipGetLastError();
   hipError_t e2 = hipFreeAsync(sums, s);
   return e != hipSuccess ? e : e2;
@@ -209,6 +241,15 @@ hipError_t run_scan(F f, uint64_t n, uint64_t base, uint64_t *oa, uint64_t *ob, 
 hipError_t launch_offsets(const uint32_t *enc_len, uint64_t n, uint64_t base, uint64_t *out_off,
                           uint64_t *cap_off, hipStream_t s) {
   return run_scan(LenVal{enc_len, n}, n, base, out_off, cap_off, s);
+}
+
+hipError_t launch_offsets_sums(const uint32_t *enc_len, uint64_t n, const uint64_t *block_sums, uint64_t base,
+                               uint64_t *out_off, uint64_t *cap_off, hipStream_t s) {
+  static_assert(kChunk == 8 * kLenSumBlock, "encode_len block sums: eight per scan chunk");
+  const uint64_t nb = (n + 1 + kChunk - 1) / kChunk;
+  scan_apply_kernel<LenVal><<<dim3((unsigned)nb), dim3(kScanBlock), 0, s>>>(LenVal{enc_len, n}, n, block_sums, 8u,
+                                                                          base, out_off, cap_off);
+  return hipGetLastError();
 }
 
 hipError_t launch_capacity(const uint64_t *in_off, uint64_t n, uint64_t base, uint64_t *cap_off,

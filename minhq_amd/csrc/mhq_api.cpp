@@ -355,6 +355,22 @@ int mhq_huff_offsets_dev(mhq_ctx *ctx, int dev, const uint32_t *enc_len, uint64_
   return hip_rc(mhq::launch_offsets(enc_len, n, base, out_off, cap_off, (hipStream_t)stream));
 }
 
+int mhq_huff_encode_layout_dev(mhq_ctx *ctx, int dev, const uint8_t *in, const uint64_t *in_off, uint64_t n,
+                               uint64_t base, uint32_t *enc_len, uint64_t *out_off, uint64_t *cap_off,
+                               void *stream) {
+  Device *d = device(ctx, dev);
+  if (!d || !out_off || (n && (!in_off || !enc_len))) return MHQ_EINVAL;
+  MHQ_TRY(hipSetDevice(d->ordinal));
+  hipStream_t s = (hipStream_t)stream;
+  const uint64_t nsums = (n + mhq::kLenSumBlock - 1) / mhq::kLenSumBlock;
+  uint64_t *sums = nullptr;
+  MHQ_TRY(hipMallocAsync((void **)&sums, (nsums ? nsums : 1) * 2 * sizeof(uint64_t), s));
+  hipError_t e = mhq::launch_encode_len(d->tables, in, in_off, 0, n, enc_len, s, sums);
+  if (e == hipSuccess) e = mhq::launch_offsets_sums(enc_len, n, sums, base, out_off, cap_off, s);
+  const hipError_t e2 = hipFreeAsync(sums, s);
+  return hip_rc(e != hipSuccess ? e : e2);
+}
+
 int mhq_huff_capacity_dev(mhq_ctx *ctx, int dev, const uint64_t *in_off, uint64_t n, uint64_t base,
                           uint64_t *cap_off, void *stream) {
   Device *d = device(ctx, dev);

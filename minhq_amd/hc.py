@@ -328,6 +328,16 @@ class Codec:
                                            cap_off.data_ptr() if cap_off is not None else None,
                                            self._stream(stream)), "offsets_dev")
 
+    def encode_layout_dev(self, data, off, enc_len, out_off, cap_off=None, base: int = 0, dev: int = 0,
+                          stream=None) -> None:
+        """encode_len_dev + offsets_dev in two launches (the scan's first pass
+        is folded into the sizing kernel)."""
+        n = off.numel() - 1
+        check(self._L.mhq_huff_encode_layout_dev(self._h, dev, data.data_ptr(), off.data_ptr(), n, base,
+                                                 enc_len.data_ptr(), out_off.data_ptr(),
+                                                 cap_off.data_ptr() if cap_off is not None else None,
+                                                 self._stream(stream)), "encode_layout_dev")
+
     def capacity_dev(self, in_off, cap_off, base: int = 0, dev: int = 0, stream=None) -> None:
         n = in_off.numel() - 1
         check(self._L.mhq_huff_capacity_dev(self._h, dev, in_off.data_ptr(), n, base, cap_off.data_ptr(),

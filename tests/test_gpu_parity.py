@@ -228,6 +228,13 @@ def _device_round_trip(codec, b):
     codec.capacity_dev(enc_off, cap2)
     torch.cuda.synchronize()
     assert torch.equal(cap2, cap_off)
+    # the fused layout call (encode_len + one scan pass) gives the same arrays
+    el3 = torch.empty_like(enc_len)
+    off3 = torch.empty_like(enc_off)
+    cap3 = torch.empty_like(cap_off)
+    codec.encode_layout_dev(data, off, el3, off3, cap3)
+    torch.cuda.synchronize()
+    assert torch.equal(el3, enc_len) and torch.equal(off3, enc_off) and torch.equal(cap3, cap_off)
 
 
 def test_device_resident_round_trip_full_size(codec):
@@ -236,6 +243,36 @@ def test_device_resident_round_trip_full_size(codec):
     from minhq_amd import workloads
 
     _device_round_trip(codec, workloads.config2())
+
+
+@pytest.mark.parametrize("n", [0, 1, 255, 256, 257, 2047, 2048, 2049, 8 * 2048 + 77, 300000])
+def test_encode_layout_matches_two_pass(codec, n):
+    """mhq_huff_encode_layout_dev against encode_len_dev + offsets_dev at the
+    block-sum edges (256-literal blocks, 2048-item scan chunks), with a base
+    and without cap_off."""
+    import torch
+
+    from minhq_amd import workloads
+
+    dev = torch.device("cuda:0")
+    b = workloads.make_batch(max(n, 1), "uniform", "hdr", lo=0, hi=64)
+    data = torch.from_numpy(b.data).to(dev)
+    off = torch.from_numpy(b.off.view(np.int64)[: n + 1].copy()).to(dev)
+    el1 = torch.full((max(n, 1),), -1, dtype=torch.int32, device=dev)
+    o1 = torch.empty(n + 1, dtype=torch.int64, device=dev)
+    c1 = torch.empty(n + 1, dtype=torch.int64, device=dev)
+    codec.encode_len_dev(data, off, el1)
+    codec.offsets_dev(el1[:n], o1, c1, base=12345)
+    el2 = torch.full((max(n, 1),), -1, dtype=torch.int32, device=dev)
+    o2 = torch.empty(n + 1, dtype=torch.int64, device=dev)
+    c2 = torch.empty(n + 1, dtype=torch.int64, device=dev)
+    codec.encode_layout_dev(data, off, el2, o2, c2, base=12345)
+    o3 = torch.empty(n + 1, dtype=torch.int64, device=dev)
+    el3 = torch.empty_like(el2)
+    codec.encode_layout_dev(data, off, el3, o3, None, base=12345)
+    torch.cuda.synchronize()
+    assert torch.equal(el1, el2) and torch.equal(o1, o2) and torch.equal(c1, c2) and torch.equal(o1, o3)
+    assert int(o1[0].item()) == 12345
 
 
 def test_device_resident_round_trip_adversarial_page_aligned(codec):

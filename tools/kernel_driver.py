@@ -96,7 +96,7 @@ def timeline_report(fn):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--kernel", default="decode", choices=["decode", "encode", "encode_len", "offsets"])
+    ap.add_argument("--kernel", default="decode", choices=["decode", "encode", "encode_len", "offsets", "layout"])
     ap.add_argument("--config", default="northstar")
     ap.add_argument("--n", type=int, default=0)
     ap.add_argument("--iters", type=int, default=50)
@@ -128,7 +128,7 @@ def main():
     torch.cuda.synchronize()
 
     per = {"decode": enc_bytes + cap_bytes + 16 * n, "encode": b.nbytes + enc_bytes + 16 * n,
-           "encode_len": b.nbytes + 12 * n, "offsets": 20 * n}[args.kernel]
+           "encode_len": b.nbytes + 12 * n, "offsets": 20 * n, "layout": b.nbytes + 32 * n}[args.kernel]
     R = max(2, int(np.ceil(args.rotate_gib * (1 << 30) / per)))
     slots = []
     for _ in range(R):
@@ -138,10 +138,12 @@ def main():
             s["out"] = torch.empty(cap_bytes + 16, dtype=torch.uint8, device=dev)
             s["len"] = torch.empty(n, dtype=torch.int32, device=dev)
             s["st"] = torch.empty(n, dtype=torch.uint8, device=dev)
-        elif args.kernel in ("encode", "encode_len"):
+        elif args.kernel in ("encode", "encode_len", "layout"):
             s["in"], s["off"], s["eoff"] = data.clone(), off.clone(), enc_off.clone()
             s["out"] = torch.empty(enc_bytes + 16, dtype=torch.uint8, device=dev)
             s["len"] = torch.empty(n, dtype=torch.int32, device=dev)
+            s["o1"] = torch.empty_like(enc_off)
+            s["o2"] = torch.empty_like(cap_off)
         else:
             s["len"] = enc_len.clone()
             s["o1"] = torch.empty_like(enc_off)
@@ -155,6 +157,8 @@ def main():
             codec.encode_dev(s["in"], s["off"], s["out"], s["eoff"])
         elif args.kernel == "encode_len":
             codec.encode_len_dev(s["in"], s["off"], s["len"])
+        elif args.kernel == "layout":
+            codec.encode_layout_dev(s["in"], s["off"], s["len"], s["o1"], s["o2"])
         else:
             codec.offsets_dev(s["len"], s["o1"], s["o2"])
 
@@ -190,7 +194,8 @@ def main():
         assert torch.equal(s["len"].long(), off[1:] - off[:-1])
     alg = {"decode": enc_bytes + b.nbytes + 16 * (n + 1) + 5 * n,
            "encode": b.nbytes + enc_bytes + 16 * (n + 1),
-           "encode_len": b.nbytes + 8 * (n + 1) + 4 * n, "offsets": 4 * n + 16 * (n + 1)}[args.kernel]
+           "encode_len": b.nbytes + 8 * (n + 1) + 4 * n, "offsets": 4 * n + 16 * (n + 1),
+           "layout": b.nbytes + 8 * (n + 1) + 8 * n + 16 * (n + 1)}[args.kernel]
     print(json.dumps({"kernel": args.kernel, "config": b.name, "n": n, "plain": b.nbytes, "enc": enc_bytes,
                       "us_per_launch": round(ms * 1e3, 2), "plain_gib_s": round(b.nbytes / ms / 1e6 / 1.073741824, 2),
                       "alg_bytes": alg, "hbm_frac": round(alg / (ms / 1e3) / 8e12, 4), "rotating": R}))
