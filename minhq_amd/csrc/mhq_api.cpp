@@ -69,7 +69,18 @@ struct Device {
   std::mutex mu;  // serialises host-memory calls (they share the staging buffers)
   hipStream_t stream = nullptr;
   Stage st[kPipe];
+  // Scratch of the device-resident calls, one buffer per caller stream: work
+  // on one stream runs in order, so a stream's buffer is reused without
+  // synchronisation (no per-call hipMallocAsync/hipFreeAsync in the stream).
+  struct Scratch {
+    hipStream_t s;
+    void *p;
+    size_t bytes;
+  };
+  std::mutex scratch_mu;
+  std::vector<Scratch> scratch;
 };
+constexpr size_t kMaxScratchStreams = 64;
 
 }  // namespace
 
@@ -130,6 +141,35 @@ void free_device(Device *d) {
   }
   if (d->stream) (void)hipStreamDestroy(d->stream);
   if (d->table_mem) (void)hipFree(d->table_mem);
+  for (auto &x : d->scratch) (void)hipFree(x.p);
+  d->scratch.clear();
+}
+
+// The scratch buffer of stream s, at least `bytes` long, or null when the
+// context already tracks kMaxScratchStreams streams (the caller then
+// allocates in stream order).  A buffer that has to grow is replaced
+// (hipFree waits for the device, so queued work that uses it is done).
+void *stream_scratch(Device *d, hipStream_t s, size_t bytes) {
+  std::lock_guard<std::mutex> g(d->scratch_mu);
+  for (auto &x : d->scratch) {
+    if (x.s != s) continue;
+    if (x.bytes >= bytes) return x.p;
+    (void)hipFree(x.p);
+    x.p = nullptr;
+    x.bytes = 0;
+    size_t b = 1;
+    while (b < bytes) b <<= 1;
+    if (hipMalloc(&x.p, b) != hipSuccess) return nullptr;
+    x.bytes = b;
+    return x.p;
+  }
+  if (d->scratch.size() >= kMaxScratchStreams) return nullptr;
+  size_t b = 65536;
+  while (b < bytes) b <<= 1;
+  void *p = nullptr;
+  if (hipMalloc(&p, b) != hipSuccess) return nullptr;
+  d->scratch.push_back(Device::Scratch{s, p, b});
+  return p;
 }
 
 Device *device(mhq_ctx *ctx, int dev) {
@@ -363,11 +403,13 @@ int mhq_huff_encode_layout_dev(mhq_ctx *ctx, int dev, const uint8_t *in, const u
   MHQ_TRY(hipSetDevice(d->ordinal));
   hipStream_t s = (hipStream_t)stream;
   const uint64_t nsums = (n + mhq::kLenSumBlock - 1) / mhq::kLenSumBlock;
-  uint64_t *sums = nullptr;
-  MHQ_TRY(hipMallocAsync((void **)&sums, (nsums ? nsums : 1) * 2 * sizeof(uint64_t), s));
+  const size_t bytes = (nsums ? nsums : 1) * 2 * sizeof(uint64_t);
+  uint64_t *sums = (uint64_t *)stream_scratch(d, s, bytes);
+  const bool own = sums == nullptr;
+  if (own) MHQ_TRY(hipMallocAsync((void **)&sums, bytes, s));
   hipError_t e = mhq::launch_encode_len(d->tables, in, in_off, 0, n, enc_len, s, sums);
   if (e == hipSuccess) e = mhq::launch_offsets_sums(enc_len, n, sums, base, out_off, cap_off, s);
-  const hipError_t e2 = hipFreeAsync(sums, s);
+  const hipError_t e2 = own ? hipFreeAsync(sums, s) : hipSuccess;
   return hip_rc(e != hipSuccess ? e : e2);
 }
 
