@@ -50,6 +50,9 @@
 #ifndef MHQ_DEC_PF  // 16-B input chunks per lane staged from registers: a wave's input slice is 1 KiB * PF
 #define MHQ_DEC_PF 4
 #endif
+#ifndef MHQ_DEC_XROUNDS  // tile rounds beyond the fewest that hold the batch (smaller tiles, more of them)
+#define MHQ_DEC_XROUNDS 0
+#endif
 #ifndef MHQ_DEC_WOUT  // a wave's output slice (bytes, multiple of 16)
 #define MHQ_DEC_WOUT 6448
 #endif
@@ -968,7 +971,7 @@ hipError_t launch_decode(const DevTables &t, const uint8_t *in, const uint64_t *
   // of tiles: no wave idles through a last, partial round.
   const uint64_t cus = (uint64_t)dev::device_cus();
   const uint64_t slots = cus * kWaves;
-  const uint64_t rounds = (n + slots * kTile - 1) / (slots * kTile);
+  const uint64_t rounds = (n + slots * kTile - 1) / (slots * kTile) + MHQ_DEC_XROUNDS;
   const uint64_t tl = std::max<uint64_t>(1, (n + slots * rounds - 1) / (slots * rounds));
   const uint64_t per_block = (((n + cus - 1) / cus + tl - 1) / tl) * tl;
   const unsigned grid = (unsigned)((n + per_block - 1) / per_block);

@@ -315,16 +315,25 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu((kT / 64 * M
 }
 
 // ---- encode_len: sum of code lengths per literal --------------------------
-// One thread per literal, reading its bytes as aligned 16-B chunks straight
-// from global memory, the first kPre of them in one go (one memory round trip
-// for a literal of up to 64 bytes; neighbouring lanes read neighbouring
-// literals, so a wave's loads cover one contiguous stretch); no staging, no
-// sort.  (A grid-stride variant with the next literal's loads in flight ran
-// slower: fewer waves hide less.)  The code lengths sit in LDS one per dword,
-// so lanes that look up different bytes rarely share a bank.  Per byte: the shifted
-// byte as address, one LDS read, the chunk's in-range mask bit times the
-// length added in.
-constexpr int kLenT = kLenSumBlock;
+// Sizes for the Auto choice and the output layout (hc/io.go:157-172: the
+// length of the temp-buffer encode, ceil(sum of code lengths / 8)).
+//
+// A wave takes 64 consecutive literals and walks their whole byte range
+// [A, B) in rounds of 1 KiB: lane l loads aligned 16-B chunk l of the round
+// (one coalesced load per lane, each byte loaded once), looks up its 16 code
+// lengths (LDS, one per dword) and forms their running sums; a wave scan of
+// the lane totals turns them into P(x) = code bits of the range's bytes
+// before x, for every byte x of the round, written to the wave's LDS row.
+// A literal [a, b) has P(b) - P(a) bits: each lane picks up P at its two
+// ends in the rounds that hold them (u32 arithmetic mod 2^32, exact for any
+// literal of < 2^32 bits).  Every lane does the same work whatever the
+// length mix, and long literals are spread over the wave.
+constexpr int kLenT = kLenSumBlock;  // 4 waves of 64 literals
+constexpr int kLenRB = 4;            // rounds whose loads are issued together
+constexpr uint32_t kRound = kWave * 16;  // bytes per round
+
+// Short literals (every one of the wave's within kPre chunks): one thread per
+// literal, its chunks loaded straight from HBM in one go.
 constexpr int kPre = 5;  // chunks loaded ahead: literals of up to 64 bytes
 
 struct LenAhead {
@@ -376,25 +385,86 @@ __device__ __forceinline__ uint32_t len_sum(const LenAhead &t, const uint8_t *__
   return bits;
 }
 
+__device__ __forceinline__ uint32_t chunk_bits(const u32x4 &x, const uint32_t *lens, uint32_t q[16]) {
+  const uint32_t w[4] = {x.x, x.y, x.z, x.w};
+  uint32_t t = 0;
+#pragma unroll
+  for (int k = 0; k < 16; k++) {
+    q[k] = t;
+    t += lens[(w[k >> 2] >> (8 * (k & 3))) & 0xffu];
+  }
+  return t;
+}
+
 __global__ __launch_bounds__(kLenT) void encode_len_kernel(const uint8_t *__restrict__ in,
                                                            const uint64_t *__restrict__ in_off, uint64_t in_bias,
                                                            uint64_t n, uint32_t *__restrict__ enc_len,
                                                            const uint8_t *__restrict__ g_len,
                                                            uint64_t *__restrict__ block_sums) {
   __shared__ uint32_t lens[256];
+  __shared__ uint32_t pw[kLenT / kWave][kRound + 4];  // P over one round (+ the position after it)
   __shared__ uint64_t part[2 * (kLenT / kWave)];
+  const uint32_t lane = threadIdx.x % kWave, wave = threadIdx.x / kWave;
+  const uint64_t s = (uint64_t)blockIdx.x * kLenT + (uint64_t)wave * kWave;  // the wave's first literal
+  const uint64_t i = s + lane;
   lens[threadIdx.x] = g_len[threadIdx.x];
+  const uint64_t a = in_off[min(i, n) + vzero()] - in_bias;
+  const uint64_t bw = in_off[min(s + kWave, n) + vzero()] - in_bias;  // end of the wave's range
   __syncthreads();
-  const uint64_t i = (uint64_t)blockIdx.x * kLenT + threadIdx.x;
   uint32_t el = 0;
-  if (i < n) {
-    LenAhead t{};
-    t.a = in_off[i] - in_bias;
-    t.b = in_off[i + 1] - in_bias;
-    len_load_chunks(t, in);
-    el = (len_sum(t, in, lens) + 7u) >> 3;
-    enc_len[i] = el;
+  if (s < n) {
+    const uint64_t nx = (uint64_t)__shfl_down((unsigned long long)a, 1);  // every lane active: lane 63 is a source
+    const uint64_t b = lane < kWave - 1 ? nx : bw;
+    const uint64_t aw = uniform64(a);  // lane 0: literal s
+    const uintptr_t base = (uintptr_t)(in + aw) & ~(uintptr_t)15;
+    const u32x4 *src = (const u32x4 *)base;
+    // aligned chunks holding a byte of [aw, bw): none for an empty range
+    const uint64_t nchunk = bw > aw ? ((uintptr_t)(in + bw) - base + 15u) >> 4 : 0u;
+    const uint32_t nround = (uint32_t)((nchunk + kWave - 1) / kWave);
+    // a wave of short literals: one thread per literal is cheaper
+    const bool lng = b > a && ((uintptr_t)(in + b) - ((uintptr_t)(in + a) & ~(uintptr_t)15) + 15u) / 16u > kPre;
+    if (__ballot(lng) == 0) {
+      LenAhead t{};
+      t.a = a;
+      t.b = b;
+      len_load_chunks(t, in);
+      el = (len_sum(t, in, lens) + 7u) >> 3;
+      if (i < n) enc_len[i] = el;
+      goto sums;
+    }
+    const uint32_t pa = (uint32_t)((uintptr_t)(in + a) - base), pb = (uint32_t)((uintptr_t)(in + b) - base);
+    uint32_t *row = pw[wave];
+    uint32_t carry = 0, Pa = 0, Pb = 0;
+    for (uint32_t r0 = 0; r0 < nround; r0 += kLenRB) {
+      u32x4 v[kLenRB];
+#pragma unroll
+      for (int k = 0; k < kLenRB; k++) {
+        const uint64_t c = (uint64_t)(r0 + k) * kWave + lane;
+        v[k] = u32x4{0u, 0u, 0u, 0u};
+        if (c < nchunk) v[k] = __builtin_nontemporal_load(src + c);  // aligned, holds a valid byte
+      }
+#pragma unroll
+      for (int k = 0; k < kLenRB; k++) {
+        if (r0 + k >= nround) break;  // wave-uniform
+        uint32_t q[16];
+        const uint32_t tot = chunk_bits(v[k], lens, q);
+        const uint32_t pre = carry + wave_incl_scan(tot) - tot;
+#pragma unroll
+        for (int j = 0; j < 16; j += 4)
+          *(u32x4 *)(row + 16u * lane + j) = u32x4{pre + q[j], pre + q[j + 1], pre + q[j + 2], pre + q[j + 3]};
+        if (lane == kWave - 1) row[kRound] = pre + tot;
+        wave_sync();
+        const uint32_t lo = (r0 + k) * kRound;  // positions [lo, lo + kRound] are in the row
+        if (pa - lo <= kRound) Pa = row[pa - lo];
+        if (pb - lo <= kRound) Pb = row[pb - lo];
+        carry = __builtin_amdgcn_readlane(pre + tot, kWave - 1);
+        wave_sync();
+      }
+    }
+    el = (Pb - Pa + 7u) >> 3;
+    if (i < n) enc_len[i] = el;
   }
+sums:
   if (!block_sums) return;  // uniform over the grid
   // the block's (sum of enc_len, sum of decode capacities) for the offsets scan
   uint64_t sa = el, sb = ((uint64_t)el * 8u) / 5u;
@@ -403,7 +473,6 @@ __global__ __launch_bounds__(kLenT) void encode_len_kernel(const uint8_t *__rest
     sa += __shfl_xor(sa, d);
     sb += __shfl_xor(sb, d);
   }
-  const int lane = threadIdx.x % kWave, wave = threadIdx.x / kWave;
   if (lane == 0) {
     part[2 * wave] = sa;
     part[2 * wave + 1] = sb;
@@ -416,7 +485,6 @@ __global__ __launch_bounds__(kLenT) void encode_len_kernel(const uint8_t *__rest
     block_sums[2 * blockIdx.x + threadIdx.x] = v;
   }
 }
-
 }  // namespace
 
 hipError_t launch_encode_len(const DevTables &t, const uint8_t *in, const uint64_t *in_off, uint64_t in_bias,

@@ -110,6 +110,23 @@ def test_random_bytes_round_trip(codec, oracle_mod):
     _check_batch(codec, oracle_mod, data, off)
 
 
+def test_encode_len_long_ranges(codec, oracle_mod):
+    """encode_len's wave-cooperative path: waves whose byte range takes many
+    1-KiB rounds (more than one batch of loads), long literals beside empty
+    and one-byte ones, and a wave of short literals next to a long one."""
+    rng = random.Random(7)
+    sizes = [0, 1, 15, 16, 17, 64, 65, 81, 1000, 5000, 70000, 0, 3, 200000]
+    lits = [bytes(rng.randrange(256) for _ in range(k)) for k in sizes]
+    lits += [bytes(rng.randrange(32, 127) for _ in range(rng.randrange(0, 60))) for _ in range(300)]
+    lits += [bytes(rng.randrange(256) for _ in range(rng.randrange(60, 400))) for _ in range(300)]
+    from minhq_amd import hc
+
+    data, off = hc.pack(lits)
+    ref = np.array([oracle_mod.encoded_len(x) for x in lits], dtype=np.uint32)
+    assert np.array_equal(codec.encode_len(data, off), ref)
+    _check_batch(codec, oracle_mod, data, off)
+
+
 def test_random_garbage_decode(codec, oracle_mod):
     """Arbitrary bytes as encoded input: exercises INVALID, partial codes and truncation."""
     from minhq_amd import hc
