@@ -10,6 +10,10 @@ through the C ABI (include/mhq_huff.h), inputs resident in HBM.  Rotating
 copies of every buffer (>= 1 GiB in all) keep the 256 MB Infinity Cache from
 serving a step's inputs from the previous step.
 
+Consecutive batches alternate over 3 HIP streams (--streams; batches are
+independent, a slot always runs on the same stream): one batch's first
+kernels fill the CUs that the previous batch's decode leaves idle at its tail.
+
 value = plaintext bytes of all ranks x steps / max-over-ranks wall time / 2^30.
 Multi-GPU: one process per GPU (torchrun); each rank owns an independent shard
 of literals (no data-path collective, weak scaling); the process group is used
@@ -106,11 +110,11 @@ def encoded_sizes(codec, batch, dev):
     return int(s.enc_off[-1].item()), int(s.cap_off[-1].item())
 
 
-def round_trip(codec, s):
+def round_trip(codec, s, stream=None):
     # encode_len + offsets scan (one call, two launches), encode, decode
-    codec.encode_layout_dev(s.data, s.off, s.enc_len, s.enc_off, s.cap_off)
-    codec.encode_dev(s.data, s.off, s.enc, s.enc_off)
-    codec.decode_dev(s.enc, s.enc_off, s.out, s.cap_off, s.out_len, s.status)
+    codec.encode_layout_dev(s.data, s.off, s.enc_len, s.enc_off, s.cap_off, stream=stream)
+    codec.encode_dev(s.data, s.off, s.enc, s.enc_off, stream=stream)
+    codec.decode_dev(s.enc, s.enc_off, s.out, s.cap_off, s.out_len, s.status, stream=stream)
 
 
 def kernel_ms(codec, slots, which, launches):
@@ -295,6 +299,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-extras", action="store_true")
+    ap.add_argument("--streams", type=int, default=3, help="streams the batches alternate over")
     ap.add_argument("--traffic", default=os.path.join(REPO, "profiles", "pmc_traffic.json"))
     args = ap.parse_args()
 
@@ -319,17 +324,31 @@ def main():
         round_trip(codec, s)
         verify_slot(s, batch)
 
+    # --streams S: consecutive batches alternate over S streams (batches are
+    # independent; a slot always runs on the same stream, so its reuse stays
+    # in stream order), letting one batch's first kernels fill the CUs that the
+    # previous batch's last kernel leaves idle at its tail
+    S = max(1, args.streams)
+    streams = [None] if S == 1 else [torch.cuda.Stream(device=dev).cuda_stream for _ in range(S)]
+    if R % S:
+        slots += [Slot(batch, enc_b, cap_b, dev) for _ in range(S - R % S)]
+        R = len(slots)
+        for s in slots:
+            round_trip(codec, s)
+            verify_slot(s, batch)
     for i in range(args.warmup):
-        round_trip(codec, slots[i % R])
+        round_trip(codec, slots[i % R], streams[i % S])
     # the timed region: K whole steps, no instrumentation between the kernels
     # (a timing event between two launches costs ~5.7 us of idle GPU)
     barrier(pg)
     t0 = time.perf_counter()
     for i in range(args.steps):
-        round_trip(codec, slots[i % R])
+        round_trip(codec, slots[i % R], streams[i % S])
     barrier(pg)
     el = time.perf_counter() - t0
     el_max = max_over_ranks(pg, el)
+    for s in slots:  # every slot's last round trip (concurrent streams) is still exact
+        verify_slot(s, batch)
     # per-kernel launch durations, live: the same slots, events only around
     # a run of back-to-back launches of one kernel on the launch stream
     enc_ms = kernel_ms(codec, slots, "encode", max(args.steps, 20))
@@ -357,7 +376,7 @@ def main():
         "data": "synthetic",
         "config": {"workload": batch.name, "literals_per_gpu": batch.n, "plain_bytes_per_gpu": batch.nbytes,
                    "encoded_bytes_per_gpu": enc_b, "step": "encode_len+offsets+encode+decode",
-                   "rotating_copies": R, "parallelism": f"shard{world} (independent literals, no collective)"},
+                   "rotating_copies": R, "streams": S, "parallelism": f"shard{world} (independent literals, no collective)"},
         "roofline": {"bound": "hbm", "kernel": "decode_kernel", "achieved": round(achieved, 2),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": traffic, "alg_bytes_per_launch": alg, "ms_per_launch": round(dec_ms, 5)},
