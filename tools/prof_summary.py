@@ -45,6 +45,35 @@ if stats:
                         r["Percentage"]])
     print(open(os.path.join(dst, f"{tag}_kernel_stats.csv")).read())
 
+# Launches that overlap no other kernel: bench.py alternates batches over
+# streams, so the step's launches share the GPU with their neighbours and
+# their spans stretch; the isolated launches (bench.py's per-kernel event runs
+# and every single-stream launch) are the ones whose duration the roofline uses.
+traces = glob.glob(os.path.join(src, "stats", "**", "*kernel_trace.csv"), recursive=True)
+if traces:
+    tr = sorted(((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"])
+                 for r in csv.DictReader(open(traces[0]))))
+    iso = defaultdict(list)
+    allk = defaultdict(list)
+    run_end = -1
+    for idx, (s0, e0, nm) in enumerate(tr):
+        k = short(nm) or nm[:60]
+        nxt = tr[idx + 1][0] if idx + 1 < len(tr) else None
+        tol = 500  # ns: same-stream back-to-back launches touch (or overlap by a few ns in the trace)
+        alone = s0 > run_end - tol and (nxt is None or nxt > e0 - tol)
+        run_end = max(run_end, e0)
+        allk[k].append(e0 - s0)
+        if alone:
+            iso[k].append(e0 - s0)
+    with open(os.path.join(dst, f"{tag}_kernel_isolated.csv"), "w", newline="") as f:
+        w = csv.writer(f)
+        w.writerow(["kernel", "calls", "avg_ns", "isolated_calls", "isolated_avg_ns", "isolated_min_ns"])
+        for k in sorted(allk, key=lambda x: -sum(allk[x])):
+            v, u = allk[k], iso.get(k, [])
+            w.writerow([k, len(v), round(sum(v) / len(v), 1), len(u), round(sum(u) / len(u), 1) if u else "",
+                        min(u) if u else ""])
+    print(open(os.path.join(dst, f"{tag}_kernel_isolated.csv")).read())
+
 bench = os.path.join(src, "bench.json")
 if os.path.exists(bench):
     shutil.copy(bench, os.path.join(dst, f"{tag}_bench.json"))
