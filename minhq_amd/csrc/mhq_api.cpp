@@ -54,8 +54,18 @@ struct Buffer {
   }
 };
 
-constexpr int kPipe = 3;                     // streams (and staging sets) per device for host-memory calls
-constexpr uint64_t kChunkBytes = 8ull << 20;  // input bytes per pipelined chunk
+#ifndef MHQ_HOST_PIPE
+#define MHQ_HOST_PIPE 4
+#endif
+#ifndef MHQ_HOST_CHUNK_MB  // encode / decode: outputs as large as the inputs, copies overlap best in small chunks
+#define MHQ_HOST_CHUNK_MB 2
+#endif
+#ifndef MHQ_HOST_LEN_CHUNK_MB  // encode_len (16 MB: encode_len alone 16 -> 27 GiB/s, but a later decode 24 -> 5, unexplained)
+#define MHQ_HOST_LEN_CHUNK_MB 2
+#endif
+constexpr int kPipe = MHQ_HOST_PIPE;  // streams (and staging sets) per device for host-memory calls
+constexpr uint64_t kChunkBytes = (uint64_t)MHQ_HOST_CHUNK_MB << 20;  // input bytes per pipelined chunk
+constexpr uint64_t kLenChunkBytes = (uint64_t)MHQ_HOST_LEN_CHUNK_MB << 20;
 
 struct Stage {
   hipStream_t s = nullptr;
@@ -237,14 +247,16 @@ int run_chunk(Device *d, Stage &S, const HostJob &j, uint64_t a, uint64_t b) {
 }
 
 // Runs literals [a, b) of a host-memory job on one device: chunks of about
-// kChunkBytes of input, pipelined over the device's kPipe stages.
+// kChunkBytes of input (kLenChunkBytes for encode_len), pipelined over the
+// device's kPipe stages.
 int run_shard(Device *d, const HostJob &j, uint64_t a, uint64_t b) {
   const uint64_t m = b - a;
   if (m == 0) return MHQ_OK;
   std::lock_guard<std::mutex> lock(d->mu);
   MHQ_TRY(hipSetDevice(d->ordinal));
   const uint64_t in_bytes = j.in_off[b] - j.in_off[a];
-  const size_t nch = (size_t)std::max<uint64_t>(1, std::min<uint64_t>(m, (in_bytes + kChunkBytes - 1) / kChunkBytes));
+  const uint64_t chunk = j.op == Op::kEncodeLen ? kLenChunkBytes : kChunkBytes;
+  const size_t nch = (size_t)std::max<uint64_t>(1, std::min<uint64_t>(m, (in_bytes + chunk - 1) / chunk));
   std::vector<uint64_t> cb = shard_bounds(j.in_off + a, m, nch);
   // staging sized for the largest chunk, before anything is enqueued
   uint64_t max_m = 0, max_in = 0, max_out = 0;

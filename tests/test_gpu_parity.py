@@ -127,6 +127,27 @@ def test_encode_len_long_ranges(codec, oracle_mod):
     _check_batch(codec, oracle_mod, data, off)
 
 
+def test_host_round_trip_many_chunks(codec):
+    """The host-memory entry points over a batch of many pipelined chunks
+    (~37 MB of plaintext, 2 MB chunks on 4 streams; encode_len in 16 MB
+    chunks): encode -> decode gives back every literal, and the encoded
+    offsets match encode_len's."""
+    from minhq_amd import hc, workloads
+
+    b = workloads.config2()
+    enc_len = codec.encode_len(b.data, b.off)
+    enc, eoff = codec.encode(b.data, b.off)
+    assert np.array_equal(np.diff(eoff), enc_len.astype(np.uint64))
+    cap = hc.capacity_offsets(eoff)
+    out, cap2, out_len, status = codec.decode(enc, eoff, cap)
+    assert not status.any()
+    assert np.array_equal(out_len.astype(np.uint64), np.diff(b.off))
+    starts = cap[:-1].astype(np.int64)
+    lens = out_len.astype(np.int64)
+    idx = np.repeat(starts - np.cumsum(lens) + lens, lens) + np.arange(int(lens.sum()))
+    assert np.array_equal(out[idx], b.data)
+
+
 def test_random_garbage_decode(codec, oracle_mod):
     """Arbitrary bytes as encoded input: exercises INVALID, partial codes and truncation."""
     from minhq_amd import hc
