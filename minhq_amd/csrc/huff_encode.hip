@@ -31,16 +31,16 @@
 #include "huff_table.h"
 
 #ifndef MHQ_ENC_T  // threads (= literals) per block tile
-#define MHQ_ENC_T 768
+#define MHQ_ENC_T 512
 #endif
 #ifndef MHQ_ENC_INCAP  // plaintext staging slice (bytes)
-#define MHQ_ENC_INCAP 32768
+#define MHQ_ENC_INCAP 24576
 #endif
 #ifndef MHQ_ENC_OUTCAP  // output staging slice (bytes, encode only)
-#define MHQ_ENC_OUTCAP 28672
+#define MHQ_ENC_OUTCAP 20480
 #endif
 #ifndef MHQ_ENC_BLOCKS  // resident workgroups per CU
-#define MHQ_ENC_BLOCKS 2
+#define MHQ_ENC_BLOCKS 3
 #endif
 
 namespace mhq {
