@@ -36,7 +36,11 @@ using dev::u32x4;
 // A thread owns kItems consecutive items; waves combine with shuffles, the
 // kWaves of a block through LDS.
 constexpr int kScanBlock = 256;
-constexpr int kItems = 8;
+#ifndef MHQ_SCAN_ITEMS  // items per thread (a multiple of 4)
+#define MHQ_SCAN_ITEMS 8
+#endif
+constexpr int kItems = MHQ_SCAN_ITEMS;
+static_assert(kItems % 4 == 0, "whole 16-B loads of lengths");
 constexpr int kChunk = kScanBlock * kItems;
 constexpr int kWaves = kScanBlock / kWave;
 
@@ -46,10 +50,12 @@ struct LenVal {  // enc_len -> (bytes, decode capacity)
   __device__ inline void load(uint64_t i0, uint64_t *a, uint64_t *b) const {
     uint32_t v[kItems];
     if (i0 + kItems <= n) {
-      const u32x4 *p = (const u32x4 *)(len + i0);  // i0 is a multiple of kItems: 32-B aligned
-      const u32x4 x = p[0], y = p[1];
-      v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w;
-      v[4] = y.x; v[5] = y.y; v[6] = y.z; v[7] = y.w;
+      const u32x4 *p = (const u32x4 *)(len + i0);  // i0 is a multiple of kItems: 16-B aligned
+#pragma unroll
+      for (int q = 0; q < kItems / 4; q++) {
+        const u32x4 x = p[q];
+        v[4 * q] = x.x; v[4 * q + 1] = x.y; v[4 * q + 2] = x.z; v[4 * q + 3] = x.w;
+      }
     } else {
 #pragma unroll
       for (int k = 0; k < kItems; k++) v[k] = i0 + k < n ? len[i0 + k] : 0u;
@@ -134,7 +140,7 @@ __global__ __launch_bounds__(kScanBlock) void scan_reduce_kernel(F f, uint64_t n
 template <class F>
 // `sums` holds (a, b) pairs for consecutive groups of kChunk / g items: the
 // reduce pass writes one per chunk (g = 1), encode_len one per block of
-// kChunk / 8 literals (g = 8).
+// kLenSumBlock literals (g = kChunk / kLenSumBlock).
 __global__ __launch_bounds__(kScanBlock) void scan_apply_kernel(F f, uint64_t n, const uint64_t *sums, uint32_t g,
                                                                  uint64_t base, uint64_t *oa, uint64_t *ob) {
   __shared__ uint64_t sh[2 * kWaves];
@@ -245,9 +251,10 @@ hipError_t launch_offsets(const uint32_t *enc_len, uint64_t n, uint64_t base, ui
 
 hipError_t launch_offsets_sums(const uint32_t *enc_len, uint64_t n, const uint64_t *block_sums, uint64_t base,
                                uint64_t *out_off, uint64_t *cap_off, hipStream_t s) {
-  static_assert(kChunk == 8 * kLenSumBlock, "encode_len block sums: eight per scan chunk");
+  static_assert(kChunk % kLenSumBlock == 0, "whole encode_len blocks per scan chunk");
   const uint64_t nb = (n + 1 + kChunk - 1) / kChunk;
-  scan_apply_kernel<LenVal><<<dim3((unsigned)nb), dim3(kScanBlock), 0, s>>>(LenVal{enc_len, n}, n, block_sums, 8u,
+  scan_apply_kernel<LenVal><<<dim3((unsigned)nb), dim3(kScanBlock), 0, s>>>(LenVal{enc_len, n}, n, block_sums,
+                                                                          (uint32_t)(kChunk / kLenSumBlock),
                                                                           base, out_off, cap_off);
   return hipGetLastError();
 }
