@@ -90,6 +90,26 @@ def test_edge_cases(codec, oracle_mod):
     assert [v for v in vals[: len(EDGE)]] == [t for _, t, _ in EDGE]
 
 
+def test_empty_batches(codec, oracle_mod):
+    """No literals, and literals that are all empty: the host-buffer entry
+    points return empty results without a launch (n == 0) or encode each
+    empty literal to zero bytes (HuffmanCompressor.Pad on nothing written,
+    hc/huffman.go:30-37) and decode it back to b"" without error."""
+    from minhq_amd import hc
+
+    assert hc.HuffmanEncodeBatch([], codec) == []
+    assert hc.HuffmanDecodeBatch([], codec) == ([], [])
+    lits = [b""] * 1000
+    enc = hc.HuffmanEncodeBatch(lits, codec)
+    assert enc == [oracle_mod.encode(b"")] * 1000 == [b""] * 1000
+    vals, errs = hc.HuffmanDecodeBatch(enc, codec)
+    assert vals == lits and errs == [None] * 1000
+    # empty literals between non-empty ones keep their slots
+    lits = [b"", b"a", b"", b"", b"www.example.com", b""] * 500
+    data, off = hc.pack(lits)
+    _check_batch(codec, oracle_mod, data, off)
+
+
 def test_every_symbol_and_long_codes(codec, oracle_mod):
     from minhq_amd import hc
 
