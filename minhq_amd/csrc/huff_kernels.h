@@ -26,8 +26,11 @@ constexpr int kLenSumBlock = 256;
 hipError_t launch_encode_len(const DevTables &t, const uint8_t *in, const uint64_t *in_off,
                              uint64_t in_bias, uint64_t n, uint32_t *enc_len, hipStream_t s,
                              uint64_t *block_sums = nullptr);
-// launch_offsets over encode_len's block sums (one pass instead of two).
-hipError_t launch_offsets_sums(const uint32_t *enc_len, uint64_t n, const uint64_t *block_sums, uint64_t base,
+// launch_offsets over encode_len's block sums (no reduce pass).  block_sums
+// is scratch of offsets_sums_scratch_bytes(n) bytes, encode_len's sums first
+// (scanned in place).
+size_t offsets_sums_scratch_bytes(uint64_t n);
+hipError_t launch_offsets_sums(const uint32_t *enc_len, uint64_t n, uint64_t *block_sums, uint64_t base,
                                uint64_t *out_off, uint64_t *cap_off, hipStream_t s);
 hipError_t launch_encode(const DevTables &t, const uint8_t *in, const uint64_t *in_off,
                          uint64_t in_bias, uint64_t n, uint8_t *out, const uint64_t *out_off,

@@ -2,24 +2,28 @@
 // arrays (encode output offsets and decode capacities).
 #include <hip/hip_runtime.h>
 
+#include <atomic>
+
 #include "huff_common.h"
 #include "huff_kernels.h"
 
 namespace mhq {
 namespace dev {
 
-int g_cus = 0;
+// CU count of the calling thread's current device, looked up once per device
+// ordinal (host threads driving different devices call this concurrently).
+constexpr int kMaxOrdinals = 64;
+std::atomic<int> g_cus[kMaxOrdinals];
 
 int device_cus() {
-  if (g_cus == 0) {
-    int d = 0, v = 0;
-    if (hipGetDevice(&d) == hipSuccess &&
-        hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, d) == hipSuccess && v > 0)
-      g_cus = v;
-    else
-      g_cus = 256;
-  }
-  return g_cus;
+  int d = 0;
+  if (hipGetDevice(&d) != hipSuccess || d < 0) d = 0;
+  std::atomic<int> *slot = d < kMaxOrdinals ? &g_cus[d] : nullptr;
+  int v = slot ? slot->load(std::memory_order_relaxed) : 0;
+  if (v > 0) return v;
+  if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, d) != hipSuccess || v <= 0) v = 256;
+  if (slot) slot->store(v, std::memory_order_relaxed);
+  return v;
 }
 
 }  // namespace dev
@@ -29,10 +33,14 @@ namespace {
 using dev::kWave;
 using dev::u32x4;
 
-// Two passes over n+1 items (item n is 0, so position n receives the total):
-//   1. block sums of (a, b) per chunk of kChunk items;
-//   2. each block adds up the sums of the chunks before it (at most a few
-//      thousand u64 pairs, read from L2), then scans its chunk and writes.
+// Three linear passes over n+1 items (item n is 0, so position n receives the
+// total):
+//   1. block sums of (a, b) per chunk of kChunk items (or encode_len's sums
+//      per kLenSumBlock literals, written by the sizing kernel itself);
+//   2. those sums scanned in superblocks of kSup, each superblock's total
+//      kept aside;
+//   3. each chunk adds the superblock totals before it (one pair per kSup
+//      sums) to its local prefix, then scans its chunk and writes.
 // A thread owns kItems consecutive items; waves combine with shuffles, the
 // kWaves of a block through LDS.
 constexpr int kScanBlock = 256;
@@ -137,39 +145,68 @@ __global__ __launch_bounds__(kScanBlock) void scan_reduce_kernel(F f, uint64_t n
   }
 }
 
+// Second pass, linear in the number of sums: superblock k (kSup consecutive
+// (a, b) pairs of `sums`, pairs at or past ns read as zero) is scanned in
+// place to exclusive prefixes within the superblock, and its total goes to
+// sup[k].  sums must hold room for ns + 1 pairs: pair ns receives the
+// superblock-local prefix of everything before it.
+constexpr int kSup = kScanBlock;
+__global__ __launch_bounds__(kScanBlock) void scan_sums_kernel(uint64_t *sums, uint64_t ns, uint64_t *sup) {
+  __shared__ uint64_t sh[2 * kWaves];
+  const int tid = threadIdx.x, lane = tid % kWave, wave = tid / kWave;
+  const uint64_t j = (uint64_t)blockIdx.x * kSup + tid;
+  const uint64_t a = j < ns ? sums[2 * j] : 0, b = j < ns ? sums[2 * j + 1] : 0;
+  const uint64_t ia = wave_incl_scan(a, lane), ib = wave_incl_scan(b, lane);
+  if (lane == kWave - 1) {
+    sh[2 * wave] = ia;
+    sh[2 * wave + 1] = ib;
+  }
+  __syncthreads();
+  uint64_t ra = ia - a, rb = ib - b, ta = 0, tb = 0;
+#pragma unroll
+  for (int w = 0; w < kWaves; w++) {
+    if (w < wave) {
+      ra += sh[2 * w];
+      rb += sh[2 * w + 1];
+    }
+    ta += sh[2 * w];
+    tb += sh[2 * w + 1];
+  }
+  if (j <= ns) {
+    sums[2 * j] = ra;
+    sums[2 * j + 1] = rb;
+  }
+  if (tid == 0) {
+    sup[2 * blockIdx.x] = ta;
+    sup[2 * blockIdx.x + 1] = tb;
+  }
+}
+
+// Third pass: chunk c's prefix is the sum of the superblock totals before its
+// superblock (at most (n+1) / (kChunk * kSup / g) pairs, a few KB at 2^24
+// items) plus the superblock-local prefix of its first pair, c*g, where `g`
+// is the number of pairs per chunk: 1 for the reduce pass, kChunk /
+// kLenSumBlock for encode_len's per-block sums.
 template <class F>
-// `sums` holds (a, b) pairs for consecutive groups of kChunk / g items: the
-// reduce pass writes one per chunk (g = 1), encode_len one per block of
-// kLenSumBlock literals (g = kChunk / kLenSumBlock).
-__global__ __launch_bounds__(kScanBlock) void scan_apply_kernel(F f, uint64_t n, const uint64_t *sums, uint32_t g,
-                                                                 uint64_t base, uint64_t *oa, uint64_t *ob) {
+__global__ __launch_bounds__(kScanBlock) void scan_apply_kernel(F f, uint64_t n, const uint64_t *sums,
+                                                                 const uint64_t *sup, uint32_t g, uint64_t base,
+                                                                 uint64_t *oa, uint64_t *ob) {
   __shared__ uint64_t sh[2 * kWaves];
   const int tid = threadIdx.x, lane = tid % kWave, wave = tid / kWave;
   // this chunk's items first: their loads are in flight during the prefix
   const uint64_t i0 = (uint64_t)blockIdx.x * kChunk + (uint64_t)tid * kItems;
   uint64_t a[kItems], b[kItems];
   f.load(i0, a, b);
-  // prefix of the chunks before this one
-  typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
-  const u64x2 *sp = (const u64x2 *)sums;
-  // (batches of eight independent loads per thread: one L2 round trip per
-  // batch, not per pair)
+  const uint64_t first = (uint64_t)blockIdx.x * g;  // this chunk's first pair
+  const uint64_t sb = first / kSup;
   uint64_t pa = 0, pb = 0;
-  const uint32_t cnt = blockIdx.x * g;
-  for (uint32_t j0 = 0; j0 < cnt; j0 += 8u * kScanBlock) {
-    u64x2 v[8];
-#pragma unroll
-    for (int k = 0; k < 8; k++) {
-      const uint32_t j = j0 + (uint32_t)k * kScanBlock + tid;
-      v[k] = j < cnt ? sp[j] : u64x2{0ull, 0ull};
-    }
-#pragma unroll
-    for (int k = 0; k < 8; k++) {
-      pa += v[k].x;
-      pb += v[k].y;
-    }
+  for (uint64_t j = tid; j < sb; j += kScanBlock) {
+    pa += sup[2 * j];
+    pb += sup[2 * j + 1];
   }
   block_sum2(pa, pb, sh);
+  pa += sums[2 * first];
+  pb += sums[2 * first + 1];
   uint64_t ta = 0, tb = 0;
 #pragma unroll
   for (int k = 0; k < kItems; k++) {
@@ -195,6 +232,7 @@ __global__ __launch_bounds__(kScanBlock) void scan_apply_kernel(F f, uint64_t n,
     ra += a[k];
     rb += b[k];
   }
+  typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
   const uint64_t c0 = (uint64_t)blockIdx.x * kChunk;
   if (c0 + kChunk <= n + 1) {
     // a whole chunk: through LDS, so each wave-wide 16-B store covers 1 KiB
@@ -228,15 +266,21 @@ __global__ __launch_bounds__(kScanBlock) void scan_apply_kernel(F f, uint64_t n,
   }
 }
 
+// Superblocks over ns pairs (pair ns included).
+inline uint64_t sup_count(uint64_t ns) { return (ns + 1 + kSup - 1) / kSup; }
+
 template <class F>
 hipError_t run_scan(F f, uint64_t n, uint64_t base, uint64_t *oa, uint64_t *ob, hipStream_t s) {
   // n+1 outputs; blocks cover indices 0..n inclusive
   const uint64_t nb = (n + 1 + kChunk - 1) / kChunk;
+  const uint64_t nsup = sup_count(nb);
   uint64_t *sums = nullptr;
-  hipError_t e = hipMallocAsync((void **)&sums, nb * 2 * sizeof(uint64_t), s);
+  hipError_t e = hipMallocAsync((void **)&sums, (nb + 1 + nsup) * 2 * sizeof(uint64_t), s);
   if (e != hipSuccess) return e;
+  uint64_t *sup = sums + 2 * (nb + 1);
   scan_reduce_kernel<F><<<dim3((unsigned)nb), dim3(kScanBlock), 0, s>>>(f, n, sums);
-  scan_apply_kernel<F><<<dim3((unsigned)nb), dim3(kScanBlock), 0, s>>>(f, n, sums, 1u, base, oa, ob);
+  scan_sums_kernel<<<dim3((unsigned)nsup), dim3(kScanBlock), 0, s>>>(sums, nb, sup);
+  scan_apply_kernel<F><<<dim3((unsigned)nb), dim3(kScanBlock), 0, s>>>(f, n, sums, sup, 1u, base, oa, ob);
   e = hipGetLastError();
   hipError_t e2 = hipFreeAsync(sums, s);
   return e != hipSuccess ? e : e2;
@@ -244,18 +288,27 @@ hipError_t run_scan(F f, uint64_t n, uint64_t base, uint64_t *oa, uint64_t *ob, 
 
 }  // namespace
 
+size_t offsets_sums_scratch_bytes(uint64_t n) {
+  const uint64_t ns = (n + kLenSumBlock - 1) / kLenSumBlock;
+  return (size_t)(ns + 1 + sup_count(ns)) * 2 * sizeof(uint64_t);
+}
+
 hipError_t launch_offsets(const uint32_t *enc_len, uint64_t n, uint64_t base, uint64_t *out_off,
                           uint64_t *cap_off, hipStream_t s) {
   return run_scan(LenVal{enc_len, n}, n, base, out_off, cap_off, s);
 }
 
-hipError_t launch_offsets_sums(const uint32_t *enc_len, uint64_t n, const uint64_t *block_sums, uint64_t base,
+hipError_t launch_offsets_sums(const uint32_t *enc_len, uint64_t n, uint64_t *block_sums, uint64_t base,
                                uint64_t *out_off, uint64_t *cap_off, hipStream_t s) {
   static_assert(kChunk % kLenSumBlock == 0, "whole encode_len blocks per scan chunk");
+  static_assert(kSup % (kChunk / kLenSumBlock) == 0, "no scan chunk straddles two superblocks");
   const uint64_t nb = (n + 1 + kChunk - 1) / kChunk;
-  scan_apply_kernel<LenVal><<<dim3((unsigned)nb), dim3(kScanBlock), 0, s>>>(LenVal{enc_len, n}, n, block_sums,
-                                                                          (uint32_t)(kChunk / kLenSumBlock),
-                                                                          base, out_off, cap_off);
+  const uint64_t ns = (n + kLenSumBlock - 1) / kLenSumBlock;
+  const uint64_t nsup = sup_count(ns);
+  uint64_t *sup = block_sums + 2 * (ns + 1);
+  scan_sums_kernel<<<dim3((unsigned)nsup), dim3(kScanBlock), 0, s>>>(block_sums, ns, sup);
+  scan_apply_kernel<LenVal><<<dim3((unsigned)nb), dim3(kScanBlock), 0, s>>>(
+      LenVal{enc_len, n}, n, block_sums, sup, (uint32_t)(kChunk / kLenSumBlock), base, out_off, cap_off);
   return hipGetLastError();
 }
 

@@ -89,6 +89,10 @@ struct Device {
   };
   std::mutex scratch_mu;
   std::vector<Scratch> scratch;
+  // Buffers a stream outgrew.  Work already queued (possibly by another
+  // thread on the same stream) may still use them, so they are freed only at
+  // mhq_close, never while a caller can hold their pointer.
+  std::vector<void *> retired;
 };
 constexpr size_t kMaxScratchStreams = 64;
 
@@ -153,23 +157,26 @@ void free_device(Device *d) {
   if (d->table_mem) (void)hipFree(d->table_mem);
   for (auto &x : d->scratch) (void)hipFree(x.p);
   d->scratch.clear();
+  for (void *p : d->retired) (void)hipFree(p);
+  d->retired.clear();
 }
 
 // The scratch buffer of stream s, at least `bytes` long, or null when the
 // context already tracks kMaxScratchStreams streams (the caller then
-// allocates in stream order).  A buffer that has to grow is replaced
-// (hipFree waits for the device, so queued work that uses it is done).
+// allocates in stream order).  A buffer that has to grow is replaced by a
+// new one and the old one retired (freed at mhq_close): another thread may
+// have just been handed it for work it is still queueing on the same stream.
 void *stream_scratch(Device *d, hipStream_t s, size_t bytes) {
   std::lock_guard<std::mutex> g(d->scratch_mu);
   for (auto &x : d->scratch) {
     if (x.s != s) continue;
     if (x.bytes >= bytes) return x.p;
-    (void)hipFree(x.p);
-    x.p = nullptr;
-    x.bytes = 0;
     size_t b = 1;
     while (b < bytes) b <<= 1;
-    if (hipMalloc(&x.p, b) != hipSuccess) return nullptr;
+    void *p = nullptr;
+    if (hipMalloc(&p, b) != hipSuccess) return nullptr;
+    d->retired.push_back(x.p);
+    x.p = p;
     x.bytes = b;
     return x.p;
   }
@@ -414,8 +421,7 @@ int mhq_huff_encode_layout_dev(mhq_ctx *ctx, int dev, const uint8_t *in, const u
   if (!d || !out_off || (n && (!in_off || !enc_len))) return MHQ_EINVAL;
   MHQ_TRY(hipSetDevice(d->ordinal));
   hipStream_t s = (hipStream_t)stream;
-  const uint64_t nsums = (n + mhq::kLenSumBlock - 1) / mhq::kLenSumBlock;
-  const size_t bytes = (nsums ? nsums : 1) * 2 * sizeof(uint64_t);
+  const size_t bytes = mhq::offsets_sums_scratch_bytes(n);
   uint64_t *sums = (uint64_t *)stream_scratch(d, s, bytes);
   const bool own = sums == nullptr;
   if (own) MHQ_TRY(hipMallocAsync((void **)&sums, bytes, s));
@@ -551,6 +557,8 @@ int mhq_read_strings(mhq_ctx *ctx, const uint8_t *blk, uint64_t blk_len, const u
   if (!d || !out_off || (n && (!blk || !pos || !limit || !prefix || !out || !out_len || !status || !next)))
     return MHQ_EINVAL;
   if (out_cap < blk_len / 5 * 8 + (blk_len % 5) * 8 / 5 + 1) return MHQ_EINVAL;
+  for (uint64_t i = 0; i < n; i++)
+    if (limit[i] > blk_len) return MHQ_EINVAL;
   std::lock_guard<std::mutex> lock(d->mu);
   MHQ_TRY(hipSetDevice(d->ordinal));
   hipStream_t s = d->stream;

@@ -32,12 +32,13 @@ struct ReadScratch {
 
 // Reader.ReadBit + Reader.ReadInt(prefix) at byte pos, bit 7-prefix being the
 // H bit, reading no byte at or past limit (hc/io.go:25-55, 73-81).
-__global__ void read_parse_kernel(const uint8_t *__restrict__ blk, const uint64_t *__restrict__ pos,
+__global__ void read_parse_kernel(const uint8_t *__restrict__ blk, uint64_t blk_len, const uint64_t *__restrict__ pos,
                                   const uint64_t *__restrict__ limit, const uint8_t *__restrict__ prefix, uint64_t n,
                                   ReadScratch sc, uint64_t *__restrict__ next) {
   const uint64_t i = (uint64_t)blockIdx.x * kT + threadIdx.x;
   if (i >= n) return;
-  const uint64_t p0 = pos[i], lim = limit[i];
+  // a limit past the block is the block's end: no byte past blk_len is read
+  const uint64_t p0 = pos[i], lim = min(limit[i], blk_len);
   const uint32_t pf = prefix[i];
   uint8_t kind = 2;
   uint64_t start = p0, take = 0, v = 0;
@@ -99,8 +100,9 @@ __global__ void gather_huff_kernel(const uint8_t *__restrict__ blk, ReadScratch 
 // Raw payloads into the output (after the decode, which zero-fills the
 // regions it stages), then the per-string outcome of hc/io.go:92-96.
 __global__ void read_finish_kernel(const uint8_t *__restrict__ blk, ReadScratch sc, uint64_t n,
-                                   const uint64_t *__restrict__ out_off, uint8_t *__restrict__ out,
-                                   uint32_t *__restrict__ out_len, uint8_t *__restrict__ status) {
+                                   const uint64_t *__restrict__ out_off, const uint64_t *__restrict__ hin_off,
+                                   uint8_t *__restrict__ out, uint32_t *__restrict__ out_len,
+                                   uint8_t *__restrict__ status) {
   const uint64_t i = (uint64_t)blockIdx.x * kT + threadIdx.x;
   if (i >= n) return;
   const uint8_t kind = sc.kind[i];
@@ -108,7 +110,9 @@ __global__ void read_finish_kernel(const uint8_t *__restrict__ blk, ReadScratch 
   uint8_t st = MHQ_STR_OK;
   uint32_t len = 0;
   if (kind == 2) {  // ReadBit / ReadInt failed: ("", nil)
-  } else if (room < sc.cap[i]) {
+  } else if (room < sc.cap[i] || hin_off[i + 1] - hin_off[i] < sc.hsz[i]) {
+    // the output region, or the packed Huffman input (overlapping payloads
+    // can total more than the block), was cut short by the buffer's end
     st = MHQ_STR_NOSPACE;
   } else if (kind == 1) {
     len = out_len[i];
@@ -409,7 +413,7 @@ hipError_t launch_read_strings(const DevTables &t, const uint8_t *blk, uint64_t 
   TRY(scratch(&sc.kind, n, s));
   TRY(scratch(&hin_off, n + 1, s));
   TRY(scratch(&hin, blk_len + 16, s));
-  read_parse_kernel<<<blocks(n), kT, 0, s>>>(blk, pos, limit, prefix, n, sc, next);
+  read_parse_kernel<<<blocks(n), kT, 0, s>>>(blk, blk_len, pos, limit, prefix, n, sc, next);
   TRY(hipGetLastError());
   // output regions: capacities back to back; the packed Huffman input
   TRY(launch_offsets(sc.cap, n, 0, out_off, nullptr, s));
@@ -419,7 +423,7 @@ hipError_t launch_read_strings(const DevTables &t, const uint8_t *blk, uint64_t 
   gather_huff_kernel<<<blocks(n), kT, 0, s>>>(blk, sc, n, hin_off, hin);
   TRY(hipGetLastError());
   TRY(launch_decode(t, hin, hin_off, 0, n, out, out_off, 0, out_len, status, s));
-  read_finish_kernel<<<blocks(n), kT, 0, s>>>(blk, sc, n, out_off, out, out_len, status);
+  read_finish_kernel<<<blocks(n), kT, 0, s>>>(blk, sc, n, out_off, hin_off, out, out_len, status);
   TRY(hipGetLastError());
 done:
   (void)hipFreeAsync(sc.start, s);

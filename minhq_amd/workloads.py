@@ -19,8 +19,8 @@ from typing import Tuple
 
 import numpy as np
 
-# netbsd.qif byte counts for 0x20..0x7E (errors.log:7-241; see
-# tests/golden/netbsd_qif.json and tests/test_workloads.py which recomputes it).
+# netbsd.qif byte counts for 0x20..0x7E (errors.log:7-241; recomputed from
+# tests/golden/netbsd_qif.json by tests/test_oracle.py::test_netbsd_histogram).
 NETBSD_HIST = [
     163, 0, 0, 0, 0, 0, 0, 0, 18, 18, 36, 1, 41, 162, 181, 165, 183, 74, 19, 0, 36, 72, 36, 0, 37, 1,
     107, 75, 0, 22, 0, 0, 0, 0, 2, 1, 1, 18, 19, 36, 0, 0, 0, 0, 0, 19, 19, 0, 2, 0, 0, 21, 37, 19,
@@ -120,17 +120,26 @@ def make_batch(n: int, length_kind: str = "uniform", dist: str = "hdr", seed: in
 
 
 # BASELINE.json configs as concrete batches.
+def count_label(n: int) -> str:
+    """2^20 -> "1M", 4*2^20 -> "4M", 2^16 -> "64K"; other sizes as digits."""
+    if n and n % (1 << 20) == 0:
+        return f"{n >> 20}M"
+    if n and n % (1 << 10) == 0:
+        return f"{n >> 10}K"
+    return str(n)
+
+
 def north_star(n: int = 1 << 20) -> Batch:
-    return make_batch(n, "uniform", "hdr", SEED_NORTH_STAR, 8, 56, "northstar-1Mx U{8..56} hdr")
+    return make_batch(n, "uniform", "hdr", SEED_NORTH_STAR, 8, 56, f"northstar-{count_label(n)}x U{{8..56}} hdr")
 
 
 def config2(n: int = 1 << 20, dist: str = "hdr") -> Batch:
-    return make_batch(n, "uniform", dist, SEED_NORTH_STAR, 8, 64, f"config2-1Mx U{{8..64}} {dist}")
+    return make_batch(n, "uniform", dist, SEED_NORTH_STAR, 8, 64, f"config2-{count_label(n)}x U{{8..64}} {dist}")
 
 
 def config4(n: int = 1 << 24) -> Batch:
-    return make_batch(n, "zipf", "hdr", SEED_ZIPF, name="config4-16Mx zipf{4..256} hdr")
+    return make_batch(n, "zipf", "hdr", SEED_ZIPF, name=f"config4-{count_label(n)}x zipf{{4..256}} hdr")
 
 
 def config5(n: int = 4 << 20) -> Batch:
-    return make_batch(n, "fixed", "adv", SEED_ADV, 128, 128, "config5-4Mx128B adv")
+    return make_batch(n, "fixed", "adv", SEED_ADV, 128, 128, f"config5-{count_label(n)}x128B adv")

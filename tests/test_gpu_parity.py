@@ -303,11 +303,13 @@ def test_device_resident_round_trip_full_size(codec):
     _device_round_trip(codec, workloads.config2())
 
 
-@pytest.mark.parametrize("n", [0, 1, 255, 256, 257, 2047, 2048, 2049, 8 * 2048 + 77, 300000])
+@pytest.mark.parametrize("n", [0, 1, 255, 256, 257, 2047, 2048, 2049, 8 * 2048 + 77, 65535, 65536, 65537,
+                               300000, 524287, 524288, 1_100_000])
 def test_encode_layout_matches_two_pass(codec, n):
     """mhq_huff_encode_layout_dev against encode_len_dev + offsets_dev at the
-    block-sum edges (256-literal blocks, 2048-item scan chunks), with a base
-    and without cap_off."""
+    block-sum edges (256-literal blocks, 2048-item scan chunks, superblocks
+    of 256 sums: 65536 literals for the layout call, 2^19 items for the
+    reduce pass), with a base and without cap_off; both against a host scan."""
     import torch
 
     from minhq_amd import workloads
@@ -331,6 +333,13 @@ def test_encode_layout_matches_two_pass(codec, n):
     torch.cuda.synchronize()
     assert torch.equal(el1, el2) and torch.equal(o1, o2) and torch.equal(c1, c2) and torch.equal(o1, o3)
     assert int(o1[0].item()) == 12345
+    el = el1[:n].cpu().numpy().astype(np.uint64)
+    ref = np.zeros(n + 1, dtype=np.uint64)
+    ref[1:] = np.cumsum(el)
+    cref = np.zeros(n + 1, dtype=np.uint64)
+    cref[1:] = np.cumsum(el * np.uint64(8) // np.uint64(5))
+    assert np.array_equal(o1.cpu().numpy().view(np.uint64), ref + np.uint64(12345))
+    assert np.array_equal(c1.cpu().numpy().view(np.uint64), cref + np.uint64(12345))
 
 
 def test_device_resident_round_trip_adversarial_page_aligned(codec):

@@ -174,3 +174,26 @@ def test_batch_drivers_match_single(oracle_mod):
     for i, x in enumerate(lits):
         assert out[int(cap[i]): int(cap[i]) + int(out_len[i])].tobytes() == x
     assert not status.any()
+
+
+def test_netbsd_histogram(golden):
+    """workloads.NETBSD_HIST (the `hdr` byte distribution) is the
+    byte histogram of the netbsd.qif header set the reference keeps in
+    errors.log:7-241 (tests/golden/netbsd_qif.json)."""
+    from minhq_amd import workloads
+
+    h = [0] * 95
+    for f in golden("netbsd_qif.json")["fields"]:
+        for s in f or ():
+            for b in s.encode():
+                h[b - 0x20] += 1
+    assert h == workloads.NETBSD_HIST and sum(h) == 5736
+
+
+def test_workload_labels():
+    from minhq_amd import workloads
+
+    assert workloads.count_label(1 << 24) == "16M" and workloads.count_label(4 << 20) == "4M"
+    assert workloads.count_label(1 << 16) == "64K" and workloads.count_label(1000) == "1000"
+    assert workloads.config4(1 << 12).name.startswith("config4-4Kx")
+    assert workloads.config5(64).name.startswith("config5-64x")

@@ -138,3 +138,28 @@ def test_read_all_prefixes(codec, oracle_mod):
             assert (vals[i], int(st[i])) == (ref, _oracle_status(rc))
             # every literal reads back, except an empty one sent Huffman-coded: io.EOF (hc/io.go:92-94)
             assert vals[i] == s and (int(st[i]) == OK or (s == b"" and int(st[i]) == EOF))
+
+
+def test_read_limit_past_block_is_einval(codec):
+    """mhq_read_strings rejects a limit past the block: the kernels
+    would otherwise read beyond the block's device copy."""
+    from minhq_amd._lib import MhqError
+
+    blk = bytes.fromhex("8bc65a283fd29c8f65127f1f")
+    with pytest.raises(MhqError):
+        codec.read_strings(blk, [0], [7], [len(blk) + 1])
+
+
+def test_read_overlapping_payloads(codec, oracle_mod):
+    """Many reads of the same literal (overlapping pos entries): the payloads
+    they share add up to more than the block, and each string is still read
+    as ReadString would, or reported as NOSPACE -- never cut silently."""
+    one = oracle_mod.write_string(b"custom-key: custom-value " * 3, prefix=7, choice=1)
+    blk = one + b"\x00" * 4
+    n = 64
+    vals, st, nxt = codec.read_strings(blk, [0] * n, [7] * n, [len(one)] * n)
+    ref, rc, used = oracle_mod.read_string(one, prefix=7)
+    assert rc == 0
+    NOSPACE = 3
+    assert all((v, int(s)) == (ref, OK) or int(s) == NOSPACE for v, s in zip(vals, st))
+    assert int(st[0]) == OK and vals[0] == ref
