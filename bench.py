@@ -15,20 +15,35 @@ independent, a slot always runs on the same stream): one batch's first
 kernels fill the CUs that the previous batch's decode leaves idle at its tail.
 
 value = plaintext bytes of all ranks x steps / max-over-ranks wall time / 2^30.
-Multi-GPU: one process per GPU (torchrun); each rank owns an independent shard
-of literals (no data-path collective, weak scaling); the process group is used
-only for the barrier and the max over ranks.
+Multi-GPU: one process per GPU.  `--gpus N` without a launcher starts N ranks
+under torch.distributed.run (a child process, before anything touches a GPU);
+under a launcher the ranks come from RANK/LOCAL_RANK/WORLD_SIZE.  Each rank
+owns an independent batch (no data-path collective, weak scaling); the
+process group carries only the barrier and the max over ranks.
 
-Extra fields (not `value`): the dominant kernel's roofline (decode), the
-north-star decode-only rate (2^20 x U{8..56}), the PCIe-inclusive host-path
-rate, and the CPU baseline (the oracle: minhq's Go algorithm restated in C,
-oracle/huff_oracle.c; there is no Go toolchain on the box).
+Extra fields (not `value`):
+  roofline            the dominant kernel (decode) against the HBM roofline;
+  long_run            the same step timed over >= 200 steps;
+  decode_only_northstar  2^20 x U{8..56} decode (the north star's shape);
+  config4_sharded     one 2^24-literal Zipf batch (BASELINE.json configs[3]),
+                      split by encoded bytes over the ranks, each rank decoding
+                      its shard device-resident; max over ranks (strong scaling);
+  config4 / config5   full-size single-GPU decode, encode and layout times
+                      (configs[3] at 2^24, configs[4] at 4 x 2^20 x 128 B), and
+                      config 5's PCIe-inclusive decode rate;
+  pcie_inclusive      host-memory ABI rates on the headline batch;
+  cpu_baseline        the oracle (minhq's Go algorithm restated in C,
+                      oracle/huff_oracle.c; no Go toolchain exists here) on 1
+                      thread and on the box's thread share, plus the
+                      table-driven CPU decoder beside it.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -43,6 +58,19 @@ GIB = float(1 << 30)
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
+
+
+def spawn_ranks(n: int) -> int:
+    """Runs this script as n ranks under torch.distributed.run (a child
+    process: nothing in this process has touched a GPU) and returns its code."""
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
+    return subprocess.call(cmd, env=env)
 
 
 def dist_setup():
@@ -117,31 +145,37 @@ def round_trip(codec, s, stream=None):
     codec.decode_dev(s.enc, s.enc_off, s.out, s.cap_off, s.out_len, s.status, stream=stream)
 
 
-def kernel_ms(codec, slots, which, launches):
-    """Mean duration of one encode or decode launch over `launches`
-    back-to-back launches rotating through the slots (HIP events on the
-    current stream, which is the one the ABI calls launch on)."""
+def events_ms(fn, launches):
+    """Mean duration of fn() over `launches` back-to-back calls on the current
+    stream (the one the ABI calls launch on), HIP events at the ends only."""
     import torch
 
-    def run(s):
-        if which == "encode":
-            codec.encode_dev(s.data, s.off, s.enc, s.enc_off)
-        else:
-            codec.decode_dev(s.enc, s.enc_off, s.out, s.cap_off, s.out_len, s.status)
-
-    for s in slots[:2]:
-        run(s)
     stream = torch.cuda.current_stream()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record(stream)
     for i in range(launches):
-        run(slots[i % len(slots)])
+        fn(i)
     e1.record(stream)
     torch.cuda.synchronize()
     return e0.elapsed_time(e1) / launches
 
 
-def verify_slot(s, batch):
+def kernel_ms(codec, slots, which, launches):
+    """Mean duration of one encode or decode launch over back-to-back launches
+    rotating through the slots."""
+    def run(i):
+        s = slots[i % len(slots)]
+        if which == "encode":
+            codec.encode_dev(s.data, s.off, s.enc, s.enc_off)
+        else:
+            codec.decode_dev(s.enc, s.enc_off, s.out, s.cap_off, s.out_len, s.status)
+
+    for i in range(2):
+        run(i)
+    return events_ms(run, launches)
+
+
+def verify_slot(s, batch=None):
     import torch
 
     torch.cuda.synchronize()
@@ -154,6 +188,16 @@ def decode_algorithmic_bytes(n, enc_bytes, plain_bytes):
     return enc_bytes + plain_bytes + 16 * (n + 1) + 5 * n
 
 
+def encode_algorithmic_bytes(n, enc_bytes, plain_bytes):
+    # SURVEY.md §8d / BASELINE.md: sum L + sum C + 8(n+1) in_off + 8(n+1) out_off + 4n enc_len
+    return plain_bytes + enc_bytes + 16 * (n + 1) + 4 * n
+
+
+def layout_algorithmic_bytes(n, plain_bytes):
+    # encode_len reads the plaintext and in_off, writes enc_len; the scan writes out_off and cap_off
+    return plain_bytes + 8 * (n + 1) + 4 * n + 16 * (n + 1)
+
+
 def load_traffic(path, kernel):
     try:
         with open(path) as f:
@@ -163,34 +207,238 @@ def load_traffic(path, kernel):
         return None
 
 
+def _threads():
+    env = os.environ.get("OMP_NUM_THREADS")
+    if env and env.isdigit() and int(env) > 0:
+        return int(env)
+    try:
+        return len(os.sched_getaffinity(0))
+    except Exception:
+        return os.cpu_count() or 1
+
+
 def cpu_baseline(batch, seconds: float):
-    """The oracle (restated Go algorithm) on the host cores: encode + decode."""
+    """The oracle (restated Go algorithm) on the host cores: encode + decode,
+    on 1 thread and on the box's thread share; the table-driven decoder
+    beside it (decode only).  Each leg runs for about seconds/4."""
     from minhq_amd import hc
     from oracle import oracle
 
     oracle.build()
-    cores = max(1, min(16, os.cpu_count() or 1))
+    cores = _threads()
     m = min(batch.n, 1 << 17)
     off = batch.off[: m + 1].copy()
     data = batch.data[: int(off[-1])].copy()
     plain = int(off[-1])
-    done = 0
+    enc_len = oracle.encode_len_batch(data, off, cores)
+    eoff = np.zeros(m + 1, dtype=np.uint64)
+    eoff[1:] = np.cumsum(enc_len, dtype=np.uint64)
+    enc = oracle.encode_batch(data, off, eoff, cores)
+    cap = hc.capacity_offsets(eoff)
+
+    def rate(fn, budget):
+        done, t0 = 0, time.perf_counter()
+        while True:
+            fn()
+            done += 1
+            el = time.perf_counter() - t0
+            if el >= budget:
+                return plain * done / el / GIB, done, el
+
+    def roundtrip(th):
+        def f():
+            el = oracle.encode_len_batch(data, off, th)
+            eo = np.zeros(m + 1, dtype=np.uint64)
+            eo[1:] = np.cumsum(el, dtype=np.uint64)
+            e = oracle.encode_batch(data, off, eo, th)
+            oracle.decode_batch(e, eo, cap, th)
+        return f
+
+    leg = max(seconds / 4.0, 0.5)
+    v_all, n_all, t_all = rate(roundtrip(cores), leg)
+    v_one, n_one, t_one = rate(roundtrip(1), leg)
+    f_all, _, _ = rate(lambda: oracle.decode_batch(enc, eoff, cap, cores, fast=True), leg / 2)
+    f_one, _, _ = rate(lambda: oracle.decode_batch(enc, eoff, cap, 1, fast=True), leg / 2)
+    d_all, _, _ = rate(lambda: oracle.decode_batch(enc, eoff, cap, cores), leg / 2)
+    return {"value": round(v_all, 4), "unit": "GiB/s", "cores": cores, "kind": "port",
+            "sample": f"first {m} literals of the workload, encode+decode, {n_all} passes in {t_all:.1f}s on "
+                      f"{cores} threads (minhq hc/huffman.go + io/bitio.go bit-serial algorithm restated in C, "
+                      f"oracle/huff_oracle.c; os.cpu_count()={os.cpu_count()})",
+            "single_thread": {"value": round(v_one, 4), "unit": "GiB/s", "passes": n_one, "seconds": round(t_one, 2)},
+            "decode_only": {"restated_go_all_threads_gib_s": round(d_all, 4),
+                            "table_driven_all_threads_gib_s": round(f_all, 4),
+                            "table_driven_single_thread_gib_s": round(f_one, 4),
+                            "note": "table-driven: a 12-bit LUT per code, tree walk for longer codes and the "
+                                    "literal end (orc_huff_decode_fast); same results as the restated loop"}}
+
+
+class Dev:
+    """Device-resident copies of one batch and its encoded form."""
+
+    def __init__(self, codec, data, off, dev):
+        import torch
+
+        self.data, self.off = data, off
+        n = off.numel() - 1
+        self.n = n
+        self.plain = int((off[-1] - off[0]).item())
+        self.enc_len = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+        self.enc_off = torch.empty(n + 1, dtype=torch.int64, device=dev)
+        self.cap_off = torch.empty(n + 1, dtype=torch.int64, device=dev)
+        codec.encode_layout_dev(data, off, self.enc_len, self.enc_off, self.cap_off)
+        torch.cuda.synchronize()
+        self.enc_bytes = int(self.enc_off[-1].item())
+        self.cap_bytes = int(self.cap_off[-1].item())
+        self.enc = torch.empty(self.enc_bytes + 16, dtype=torch.uint8, device=dev)
+        codec.encode_dev(data, off, self.enc, self.enc_off)
+        torch.cuda.synchronize()
+
+
+def decode_slots(dv, lo, hi, rotate_bytes, dev):
+    """Rotating decode buffers for literals [lo, hi) of a Dev batch: the
+    encoded bytes and rebased offsets copied R times (R copies >= rotate_bytes)."""
+    import torch
+
+    a, b = int(dv.enc_off[lo].item()), int(dv.enc_off[hi].item())
+    ca, cb = int(dv.cap_off[lo].item()), int(dv.cap_off[hi].item())
+    per = (b - a) + (cb - ca) + 16 * (hi - lo + 1) + 5 * (hi - lo)
+    R = max(1, int(np.ceil(rotate_bytes / max(per, 1))))
+    slots = []
+    for _ in range(R):
+        s = type("S", (), {})()
+        s.enc = dv.enc[a:b + 16].clone()
+        s.enc_off = dv.enc_off[lo:hi + 1] - a
+        s.cap_off = dv.cap_off[lo:hi + 1] - ca
+        s.out = torch.empty(cb - ca + 16, dtype=torch.uint8, device=dev)
+        s.out_len = torch.empty(max(hi - lo, 1), dtype=torch.int32, device=dev)
+        s.status = torch.empty(max(hi - lo, 1), dtype=torch.uint8, device=dev)
+        slots.append(s)
+    return slots
+
+
+def check_decode(dv, lo, hi, s):
+    """The decode of literals [lo, hi) reproduces the plaintext (on the device)."""
+    import torch
+
+    torch.cuda.synchronize()
+    n = hi - lo
+    if n == 0:
+        return
+    assert int(s.status[:n].sum().item()) == 0, "INVALID on encoder output"
+    lens = (dv.off[lo + 1:hi + 1] - dv.off[lo:hi])
+    assert torch.equal(s.out_len[:n].long(), lens), "length mismatch"
+    starts = s.cap_off[:-1]
+    rep = torch.repeat_interleave(starts, lens)
+    within = torch.arange(int(lens.sum().item()), device=lens.device) - torch.repeat_interleave(
+        torch.cumsum(lens, 0) - lens, lens)
+    p0 = int(dv.off[lo].item())
+    assert torch.equal(s.out[rep + within], dv.data[p0:p0 + int(lens.sum().item())]), "byte mismatch"
+
+
+def config4_sharded(codec, dev, world, rank, pg, launches, rotate_bytes):
+    """BASELINE.json configs[3]: one 2^24-literal Zipf batch split over the
+    ranks by encoded bytes; each rank decodes its shard device-resident."""
+    import torch
+
+    from minhq_amd import shard, workloads
+
+    n = 1 << 24
+    data, off = workloads.make_batch_device(n, "zipf", "hdr", workloads.SEED_ZIPF, device=dev)
+    dv = Dev(codec, data, off, dev)
+    parts = shard.plan_shards_device(dv.enc_off, world)
+    lo, hi = parts[rank]
+    slots = decode_slots(dv, lo, hi, rotate_bytes, dev)
+
+    def run(i):
+        s = slots[i % len(slots)]
+        codec.decode_dev(s.enc, s.enc_off, s.out, s.cap_off, s.out_len, s.status)
+
+    run(0)
+    check_decode(dv, lo, hi, slots[0])
+    barrier(pg)
+    ms = events_ms(run, launches)
+    barrier(pg)
+    ms_max = max_over_ranks(pg, ms)
+    alg = decode_algorithmic_bytes(n, dv.enc_bytes, dv.plain)
+    res = {"workload": f"config4: {n} literals Zipf{{4..256}} hdr, one batch split by encoded bytes",
+           "literals": n, "plain_bytes": dv.plain, "encoded_bytes": dv.enc_bytes, "ranks": world,
+           "shard_literals_rank0": parts[0][1] - parts[0][0],
+           "ms_per_launch_max_over_ranks": round(ms_max, 5),
+           "gib_s": round(dv.plain / (ms_max / 1e3) / GIB, 2),
+           "hbm_frac_aggregate": round(alg / (ms_max / 1e3) / 1e9 / (HBM_PEAK_GBS * world), 4),
+           "scaling": "strong", "rotating_copies": len(slots)}
+    if world == 1:  # full-size single-GPU times of the other kernels
+        plain_alg = layout_algorithmic_bytes(n, dv.plain)
+        enc_ms = events_ms(lambda i: codec.encode_dev(data, off, dv.enc, dv.enc_off), max(4, launches // 2))
+        lay_ms = events_ms(lambda i: codec.encode_layout_dev(data, off, dv.enc_len, dv.enc_off, dv.cap_off),
+                           max(4, launches // 2))
+        res["decode_hbm_frac"] = round(alg / (ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4)
+        res["encode_ms"] = round(enc_ms, 5)
+        res["encode_hbm_frac"] = round(encode_algorithmic_bytes(n, dv.enc_bytes, dv.plain) / (enc_ms / 1e3) / 1e9
+                                       / HBM_PEAK_GBS, 4)
+        res["layout_ms"] = round(lay_ms, 5)
+        res["layout_hbm_frac"] = round(plain_alg / (lay_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4)
+    del slots, dv, data, off
+    torch.cuda.empty_cache()
+    return res
+
+
+def config5(codec, dev, launches, rotate_bytes):
+    """BASELINE.json configs[4]: 4 x 2^20 literals of 128 bytes whose codes are
+    >= 26 bits; 1-GPU decode roofline and the PCIe-inclusive decode rate."""
+    import torch
+
+    from minhq_amd import hc, workloads
+
+    n = 4 << 20
+    data, off = workloads.make_batch_device(n, "fixed", "adv", workloads.SEED_ADV, 128, 128, device=dev)
+    dv = Dev(codec, data, off, dev)
+    slots = decode_slots(dv, 0, n, rotate_bytes, dev)
+
+    def run(i):
+        s = slots[i % len(slots)]
+        codec.decode_dev(s.enc, s.enc_off, s.out, s.cap_off, s.out_len, s.status)
+
+    run(0)
+    check_decode(dv, 0, n, slots[0])
+    ms = events_ms(run, launches)
+    alg = decode_algorithmic_bytes(n, dv.enc_bytes, dv.plain)
+    enc_ms = events_ms(lambda i: codec.encode_dev(data, off, dv.enc, dv.enc_off), max(4, launches // 2))
+    lay_ms = events_ms(lambda i: codec.encode_layout_dev(data, off, dv.enc_len, dv.enc_off, dv.cap_off),
+                       max(4, launches // 2))
+    res = {"workload": f"config5: {n} literals x 128 B, bytes with >= 26-bit codes", "literals": n,
+           "plain_bytes": dv.plain, "encoded_bytes": dv.enc_bytes,
+           "decode_ms": round(ms, 5), "decode_gib_s": round(dv.plain / (ms / 1e3) / GIB, 2),
+           "decode_hbm_frac": round(alg / (ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
+           "encode_ms": round(enc_ms, 5),
+           "encode_hbm_frac": round(encode_algorithmic_bytes(n, dv.enc_bytes, dv.plain) / (enc_ms / 1e3) / 1e9
+                                    / HBM_PEAK_GBS, 4),
+           "layout_ms": round(lay_ms, 5), "rotating_copies": len(slots)}
+    # PCIe-inclusive decode: pinned host input (encoded bytes, offsets), pinned host outputs
+    enc_h = torch.empty(dv.enc_bytes, dtype=torch.uint8).pin_memory()
+    enc_h.copy_(dv.enc[:dv.enc_bytes])
+    eoff_h = torch.empty(n + 1, dtype=torch.int64).pin_memory()
+    eoff_h.copy_(dv.enc_off)
+    cap_h = torch.empty(n + 1, dtype=torch.int64).pin_memory()
+    cap_h.copy_(dv.cap_off)
+    out_h = torch.empty(dv.cap_bytes + 16, dtype=torch.uint8).pin_memory()
+    len_h = torch.empty(n, dtype=torch.int32).pin_memory()
+    st_h = torch.empty(n, dtype=torch.uint8).pin_memory()
+    del slots
+    torch.cuda.empty_cache()
+    pool = iter([out_h.numpy(), len_h.numpy().view(np.uint8), st_h.numpy()] * 2)
+    alloc = lambda nb: next(pool)  # noqa: E731  (the pinned outputs, in the order decode asks for them)
+    e, eo, co = enc_h.numpy(), eoff_h.numpy().view(np.uint64), cap_h.numpy().view(np.uint64)
+    codec.decode(e, eo, co, alloc=alloc)  # warm: staging buffers
     t0 = time.perf_counter()
-    while True:
-        enc_len = oracle.encode_len_batch(data, off, cores)
-        eoff = np.zeros(m + 1, dtype=np.uint64)
-        eoff[1:] = np.cumsum(enc_len, dtype=np.uint64)
-        enc = oracle.encode_batch(data, off, eoff, cores)
-        cap = hc.capacity_offsets(eoff)
-        oracle.decode_batch(enc, eoff, cap, cores)
-        done += 1
-        el = time.perf_counter() - t0
-        if el >= seconds:
-            break
-    return {"value": round(plain * done / el / GIB, 4), "unit": "GiB/s", "cores": cores, "kind": "port",
-            "sample": f"first {m} literals of the workload, encode+decode x{done} passes in {el:.1f}s "
-                      f"({cores} threads; minhq hc/huffman.go + io/bitio.go bit-serial algorithm "
-                      f"restated in C, oracle/huff_oracle.c)"}
+    _, _, out_len, status = codec.decode(e, eo, co, alloc=alloc)
+    t1 = time.perf_counter()
+    assert not status.any() and np.array_equal(out_len.astype(np.int64), np.full(n, 128))
+    res["pcie_inclusive_decode_gib_s"] = round(dv.plain / (t1 - t0) / GIB, 3)
+    res["pcie_note"] = "host-memory mhq_huff_decode, pinned input and outputs, 2 MB chunks pipelined on 4 streams"
+    del dv, data, off
+    torch.cuda.empty_cache()
+    return res
 
 
 def decode_only(codec, dev, steps, warmup, rotate_bytes):
@@ -200,38 +448,25 @@ def decode_only(codec, dev, steps, warmup, rotate_bytes):
     from minhq_amd import workloads
 
     b = workloads.north_star()
-    enc_b, cap_b = encoded_sizes(codec, b, dev)
-    base = Slot(b, enc_b, cap_b, dev)
-    round_trip(codec, base)
-    verify_slot(base, b)
-    per = base.enc.numel() + base.enc_off.numel() * 16 + base.out.numel() + b.n * 5
-    R = max(2, int(np.ceil(rotate_bytes / per)))
-    slots = []
-    for _ in range(R):
-        s = type("S", (), {})()
-        s.enc = base.enc.clone()
-        s.enc_off = base.enc_off.clone()
-        s.cap_off = base.cap_off.clone()
-        s.out = torch.empty_like(base.out)
-        s.out_len = torch.empty_like(base.out_len)
-        s.status = torch.empty_like(base.status)
-        slots.append(s)
+    data = torch.from_numpy(b.data).to(dev)
+    off = torch.from_numpy(b.off.view(np.int64)).to(dev)
+    dv = Dev(codec, data, off, dev)
+    slots = decode_slots(dv, 0, b.n, rotate_bytes, dev)
+
+    def run(i):
+        s = slots[i % len(slots)]
+        codec.decode_dev(s.enc, s.enc_off, s.out, s.cap_off, s.out_len, s.status)
+
+    run(0)
+    check_decode(dv, 0, b.n, slots[0])
     for i in range(warmup):
-        s = slots[i % R]
-        codec.decode_dev(s.enc, s.enc_off, s.out, s.cap_off, s.out_len, s.status)
-    torch.cuda.synchronize()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    for i in range(steps):
-        s = slots[i % R]
-        codec.decode_dev(s.enc, s.enc_off, s.out, s.cap_off, s.out_len, s.status)
-    e1.record()
-    torch.cuda.synchronize()
-    ms = e0.elapsed_time(e1) / steps
-    alg = decode_algorithmic_bytes(b.n, enc_b, b.nbytes)
-    return {"workload": b.name, "literals": b.n, "plain_bytes": b.nbytes, "encoded_bytes": enc_b,
+        run(i)
+    ms = events_ms(run, steps)
+    alg = decode_algorithmic_bytes(b.n, dv.enc_bytes, b.nbytes)
+    return {"workload": b.name, "literals": b.n, "plain_bytes": b.nbytes, "encoded_bytes": dv.enc_bytes,
             "ms_per_launch": round(ms, 5), "gib_s": round(b.nbytes / (ms / 1e3) / GIB, 3),
-            "hbm_frac": round(alg / (ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4), "rotating_copies": R}
+            "hbm_frac": round(alg / (ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4), "alg_bytes_per_launch": alg,
+            "rotating_copies": len(slots)}
 
 
 class PinnedPool:
@@ -296,12 +531,17 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--literals", type=int, default=1 << 20)
     ap.add_argument("--rotate-gib", type=float, default=1.0, help="total bytes of rotating buffer copies")
-    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--cpu-seconds", type=float, default=16.0)
+    ap.add_argument("--long-steps", type=int, default=200, help="steps of the extra long_run timing (0: skip)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-extras", action="store_true")
+    ap.add_argument("--no-configs", action="store_true", help="skip the full-size configs 4 and 5")
     ap.add_argument("--streams", type=int, default=3, help="streams the batches alternate over")
     ap.add_argument("--traffic", default=os.path.join(REPO, "profiles", "pmc_traffic.json"))
     args = ap.parse_args()
+
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        raise SystemExit(spawn_ranks(args.gpus))
 
     import torch
 
@@ -311,6 +551,8 @@ def main():
     if not os.path.exists(mbuild.LIB):
         mbuild.build()
     world, rank, local, pg = dist_setup()
+    if world != args.gpus and rank == 0:
+        log(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; measuring {world} rank(s)")
     dev = torch.device("cuda", local)
     codec = hc.Codec(devices=[local])
 
@@ -322,7 +564,7 @@ def main():
     slots = [first] + [Slot(batch, enc_b, cap_b, dev) for _ in range(R - 1)]
     for s in slots:  # correctness gate before timing
         round_trip(codec, s)
-        verify_slot(s, batch)
+        verify_slot(s)
 
     # --streams S: consecutive batches alternate over S streams (batches are
     # independent; a slot always runs on the same stream, so its reuse stays
@@ -335,7 +577,7 @@ def main():
         R = len(slots)
         for s in slots:
             round_trip(codec, s)
-            verify_slot(s, batch)
+            verify_slot(s)
     for i in range(args.warmup):
         round_trip(codec, slots[i % R], streams[i % S])
     # the timed region: K whole steps, no instrumentation between the kernels
@@ -348,11 +590,24 @@ def main():
     el = time.perf_counter() - t0
     el_max = max_over_ranks(pg, el)
     for s in slots:  # every slot's last round trip (concurrent streams) is still exact
-        verify_slot(s, batch)
+        verify_slot(s)
+    long_run = None
+    if args.long_steps > 0 and not args.no_extras:
+        barrier(pg)
+        t0 = time.perf_counter()
+        for i in range(args.long_steps):
+            round_trip(codec, slots[i % R], streams[i % S])
+        barrier(pg)
+        el_long = max_over_ranks(pg, time.perf_counter() - t0)
+        for s in slots:
+            verify_slot(s)
+        long_run = {"steps": args.long_steps, "seconds": round(el_long, 5),
+                    "value": round(batch.nbytes * world * args.long_steps / el_long / GIB, 3),
+                    "ms_per_step": round(el_long / args.long_steps * 1e3, 5)}
     # per-kernel launch durations, live: the same slots, events only around
     # a run of back-to-back launches of one kernel on the launch stream
-    enc_ms = kernel_ms(codec, slots, "encode", max(args.steps, 20))
-    dec_ms = kernel_ms(codec, slots, "decode", max(args.steps, 20))
+    enc_ms = kernel_ms(codec, slots, "encode", max(args.steps, 50))
+    dec_ms = kernel_ms(codec, slots, "decode", max(args.steps, 50))
 
     plain_total = batch.nbytes * world * args.steps
     value = plain_total / el_max / GIB
@@ -377,14 +632,26 @@ def main():
         "config": {"workload": batch.name, "literals_per_gpu": batch.n, "plain_bytes_per_gpu": batch.nbytes,
                    "encoded_bytes_per_gpu": enc_b, "step": "encode_len+offsets+encode+decode",
                    "rotating_copies": R, "streams": S, "parallelism": f"shard{world} (independent literals, no collective)"},
-        "roofline": {"bound": "hbm", "kernel": "decode_kernel", "achieved": round(achieved, 2),
+        "roofline": {"bound": "hbm", "kernel": "decode", "achieved": round(achieved, 2),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                     "traffic": traffic, "alg_bytes_per_launch": alg, "ms_per_launch": round(dec_ms, 5)},
+                     "traffic": traffic, "traffic_source": os.path.relpath(args.traffic, REPO),
+                     "alg_bytes_per_launch": alg, "ms_per_launch": round(dec_ms, 5)},
         "encode_ms_per_launch": round(enc_ms, 5),
+        "encode_hbm_frac": round(encode_algorithmic_bytes(batch.n, enc_b, batch.nbytes) / (enc_ms / 1e3) / 1e9
+                                 / HBM_PEAK_GBS, 4),
     }
+    if long_run:
+        res["long_run"] = long_run
+    del slots
+    torch.cuda.empty_cache()
+    if not args.no_extras and not args.no_configs:
+        res["config4_sharded"] = config4_sharded(codec, dev, world, rank, pg, max(args.steps, 20),
+                                                 args.rotate_gib * GIB)
     if rank == 0 and world == 1 and not args.no_extras:
-        res["decode_only_northstar"] = decode_only(codec, dev, max(args.steps, 20), args.warmup,
+        res["decode_only_northstar"] = decode_only(codec, dev, max(args.steps, 50), args.warmup,
                                                    args.rotate_gib * GIB)
+        if not args.no_configs:
+            res["config5"] = config5(codec, dev, max(args.steps, 10), args.rotate_gib * GIB)
         res["pcie_inclusive"] = pcie_inclusive(codec, batch)
     if rank == 0 and world == 1 and not args.no_cpu:
         res["cpu_baseline"] = cpu_baseline(batch, args.cpu_seconds)

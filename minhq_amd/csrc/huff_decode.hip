@@ -966,6 +966,9 @@ hipError_t launch_decode(const DevTables &t, const uint8_t *in, const uint64_t *
                          uint64_t n, uint8_t *out, const uint64_t *out_off, uint64_t out_bias,
                          uint32_t *out_len, uint8_t *status, hipStream_t s) {
   if (n == 0) return hipSuccess;
+#ifdef MHQ_DEC_WG
+  return launch_decode_wg(t, in, in_off, in_bias, n, out, out_off, out_bias, out_len, status, s);
+#endif
   // One workgroup per CU, each a contiguous range of whole wave tiles.  The
   // tile length (<= kTile) is chosen so that every wave gets the same number
   // of tiles: no wave idles through a last, partial round.

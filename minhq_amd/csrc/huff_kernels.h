@@ -38,6 +38,10 @@ hipError_t launch_encode(const DevTables &t, const uint8_t *in, const uint64_t *
 hipError_t launch_decode(const DevTables &t, const uint8_t *in, const uint64_t *in_off,
                          uint64_t in_bias, uint64_t n, uint8_t *out, const uint64_t *out_off,
                          uint64_t out_bias, uint32_t *out_len, uint8_t *status, hipStream_t s);
+// The workgroup-cooperative decode (huff_decode_wg.hip); same contract.
+hipError_t launch_decode_wg(const DevTables &t, const uint8_t *in, const uint64_t *in_off,
+                            uint64_t in_bias, uint64_t n, uint8_t *out, const uint64_t *out_off,
+                            uint64_t out_bias, uint32_t *out_len, uint8_t *status, hipStream_t s);
 // out_off[i] = base + sum_{j<i} enc_len[j]; cap_off[i] = base + sum_{j<i} floor(8*enc_len[j]/5)
 // (either output may be null).  Scratch comes from hipMallocAsync on `s`.
 hipError_t launch_offsets(const uint32_t *enc_len, uint64_t n, uint64_t base, uint64_t *out_off,

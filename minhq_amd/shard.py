@@ -64,3 +64,22 @@ def max_over_ranks(pg, x: float, device: str = "cpu") -> float:
     t = torch.tensor([float(x)], dtype=torch.float64, device=device)
     pg.all_reduce(t, op=pg.ReduceOp.MAX)
     return float(t.item())
+
+
+def plan_shards_device(off, parts: int):
+    """plan_shards on a device tensor of offsets (int64, n+1 entries), without
+    copying the offsets to the host: the same cuts, as a list of (lo, hi)."""
+    import torch
+
+    if parts < 1:
+        raise ValueError("parts must be >= 1")
+    n = off.numel() - 1
+    if n <= 0:
+        return [(0, 0)] * parts
+    base, total = int(off[0].item()), int((off[-1] - off[0]).item())
+    targets = torch.tensor([base + (total * k) // parts for k in range(1, parts)], dtype=torch.int64,
+                           device=off.device)
+    cuts = [0] + [int(c) for c in torch.searchsorted(off, targets, right=False).tolist()] + [n]
+    for k in range(1, parts):
+        cuts[k] = min(max(cuts[k], cuts[k - 1]), n)
+    return [(cuts[k], cuts[k + 1]) for k in range(parts)]

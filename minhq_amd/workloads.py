@@ -143,3 +143,61 @@ def config4(n: int = 1 << 24) -> Batch:
 
 def config5(n: int = 4 << 20) -> Batch:
     return make_batch(n, "fixed", "adv", SEED_ADV, 128, 128, f"config5-{count_label(n)}x128B adv")
+
+
+# ---- the same batches generated on a device (torch) ------------------------
+# Bit-identical to make_batch: splitmix64 in wrapping int64 arithmetic
+# (logical shifts by masking), the same float64 unit values and CDFs.  Used for
+# the full-size configs (2^24 literals), which numpy builds in minutes.
+def _splitmix64_t(torch, seed: int, count: int, start: int, device):
+    idx = torch.arange(start + 1, start + count + 1, dtype=torch.int64, device=device)
+
+    def s64(x):  # an unsigned 64-bit constant as the int64 with the same bits
+        x &= 0xFFFFFFFFFFFFFFFF
+        return x - (1 << 64) if x >= (1 << 63) else x
+
+    def shr(z, k):  # logical right shift
+        return (z >> k) & ((1 << (64 - k)) - 1)
+
+    z = idx * s64(0x9E3779B97F4A7C15) + s64(seed)
+    z = (z ^ shr(z, 30)) * s64(0xBF58476D1CE4E5B9)
+    z = (z ^ shr(z, 27)) * s64(0x94D049BB133111EB)
+    return z ^ shr(z, 31)
+
+
+def _unit_t(torch, r):
+    return ((r >> 11) & ((1 << 53) - 1)).to(torch.float64) * (1.0 / (1 << 53))
+
+
+def make_batch_device(n: int, length_kind: str = "uniform", dist: str = "hdr", seed: int = SEED_NORTH_STAR,
+                      lo: int = 8, hi: int = 56, device="cuda", chunk: int = 1 << 26):
+    """make_batch's literals as device tensors (data u8, off int64[n+1])."""
+    import torch
+
+    r = _splitmix64_t(torch, seed, n, 0, device)
+    if length_kind == "uniform":
+        span = hi - lo + 1
+        rh, rl = (r >> 32) & 0xFFFFFFFF, r & 0xFFFFFFFF  # unsigned r mod span, in int64
+        L = lo + ((rh % span) * ((1 << 32) % span) + rl % span) % span
+    elif length_kind == "fixed":
+        L = torch.full((n,), lo, dtype=torch.int64, device=device)
+    elif length_kind == "zipf":
+        ks = np.arange(4, 257)
+        cdf = np.cumsum(1.0 / (ks - 3))
+        cdf /= cdf[-1]
+        i = torch.searchsorted(torch.from_numpy(cdf).to(device), _unit_t(torch, r), right=True)
+        L = torch.from_numpy(ks).to(device)[i.clamp(0, len(ks) - 1)]
+    else:
+        raise ValueError(length_kind)
+    del r
+    off = torch.zeros(n + 1, dtype=torch.int64, device=device)
+    torch.cumsum(L, 0, out=off[1:])
+    total = int(off[-1].item())
+    syms, cdf = byte_alphabet(dist)
+    syms_t, cdf_t = torch.from_numpy(syms).to(device), torch.from_numpy(cdf).to(device)
+    data = torch.empty(total, dtype=torch.uint8, device=device)
+    for a in range(0, total, chunk):
+        b = min(total, a + chunk)
+        u = _unit_t(torch, _splitmix64_t(torch, seed ^ _BYTE_STREAM_XOR, b - a, a, device))
+        data[a:b] = syms_t[torch.searchsorted(cdf_t, u, right=True).clamp(0, len(syms) - 1)]
+    return data, off

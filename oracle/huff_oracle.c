@@ -110,6 +110,32 @@ static int32_t make_layer(uint32_t prefix, uint8_t prefix_len) {
   return layer;
 }
 
+/* Table-driven decode (CPU baseline beside the restated Go loop):
+ * g_fast[w] is the symbol and length of the code (<= ORC_FAST_BITS bits) that
+ * starts the ORC_FAST_BITS-bit window w, found by walking the same tree; 0 if
+ * the code is longer (then the tree walk takes over). */
+#define ORC_FAST_BITS 12
+typedef struct {
+  uint8_t sym, len;
+} orc_fast;
+static orc_fast g_fast[1u << ORC_FAST_BITS];
+
+static void build_fast_lut(void) {
+  for (uint32_t w = 0; w < (1u << ORC_FAST_BITS); w++) {
+    int32_t node = g_root;
+    g_fast[w].len = 0;
+    for (int b = 0; b < ORC_FAST_BITS; b++) {
+      node = g_nodes[node].next[(w >> (ORC_FAST_BITS - 1 - b)) & 1u];
+      if (node < 0) break;
+      if (g_nodes[node].leaf) {
+        g_fast[w].sym = g_nodes[node].val;
+        g_fast[w].len = (uint8_t)(b + 1);
+        break;
+      }
+    }
+  }
+}
+
 /* The reference initialises lazily and without synchronisation
  * (hc/huffman.go:81-87); here it is built exactly once (pthread_once) so the
  * threaded CPU baseline is race free. */
@@ -136,6 +162,7 @@ static void init_once(void) {
   }
   g_nnodes = 0;
   g_root = make_layer(0, 0);
+  build_fast_lut();
 }
 
 void orc_init(void) { pthread_once(&g_once, init_once); }
@@ -297,6 +324,49 @@ int orc_huff_decode(const uint8_t *in, size_t len, uint8_t *out, size_t cap, siz
     }
   }
   *out_len = i;
+  return ORC_OK;
+}
+
+/* Same results as orc_huff_decode, a table lookup per code of <= 12 bits:
+ * the next 12 bits (zeros past the end) index g_fast; a code that fits the
+ * literal is taken whole, anything else (a longer code, the end of the
+ * literal, the EOS prefix) goes one symbol through the bit-serial tree walk,
+ * so the end-of-literal, INVALID and buffer-full rules are the reference's. */
+int orc_huff_decode_fast(const uint8_t *in, size_t len, uint8_t *out, size_t cap, size_t *out_len) {
+  orc_init();
+  const uint64_t end = (uint64_t)len * 8u;
+  uint64_t pos = 0;
+  size_t n = 0;
+  while (n < cap && pos < end) {
+    /* 32 bits from pos, MSB first, zeros past the end */
+    const uint64_t byte = pos >> 3;
+    uint64_t v = 0;
+    for (int k = 0; k < 5; k++) v = (v << 8) | (byte + (uint64_t)k < len ? in[byte + (uint64_t)k] : 0u);
+    const uint32_t win = (uint32_t)(v >> (8u - (pos & 7u)));
+    const orc_fast e = g_fast[win >> (32 - ORC_FAST_BITS)];
+    if (e.len && (uint64_t)e.len <= end - pos) {
+      out[n++] = e.sym;
+      pos += e.len;
+      continue;
+    }
+    int32_t node = g_root; /* one symbol, bit by bit (hc/huffman.go:104-119) */
+    for (;;) {
+      if (pos >= end) goto done; /* EOF inside a code: partial code dropped */
+      const uint32_t bit = (in[pos >> 3] >> (7u - (pos & 7u))) & 1u;
+      pos++;
+      node = g_nodes[node].next[bit];
+      if (node < 0) {
+        *out_len = n;
+        return ORC_INVALID;
+      }
+      if (g_nodes[node].leaf) {
+        out[n++] = g_nodes[node].val;
+        break;
+      }
+    }
+  }
+done:
+  *out_len = n;
   return ORC_OK;
 }
 
@@ -561,7 +631,7 @@ int orc_write_string(const uint8_t *s, size_t len, uint8_t lead, uint8_t lead_bi
 /* the restated Go loop above.                                               */
 /* ------------------------------------------------------------------------ */
 typedef struct {
-  int op; /* 0 len, 1 encode, 2 decode */
+  int op; /* 0 len, 1 encode, 2 decode, 3 table-driven decode */
   const uint8_t *in;
   const uint64_t *in_off;
   uint8_t *out;
@@ -586,7 +656,8 @@ static void *orc_worker(void *arg) {
       if (err) j->rc = err;
     } else {
       size_t cap = (size_t)(j->out_off[i + 1] - j->out_off[i]), got = 0;
-      int st = orc_huff_decode(src, n, j->out + j->out_off[i], cap, &got);
+      int st = j->op == 2 ? orc_huff_decode(src, n, j->out + j->out_off[i], cap, &got)
+                          : orc_huff_decode_fast(src, n, j->out + j->out_off[i], cap, &got);
       j->lens[i] = (uint32_t)got;
       j->status[i] = (uint8_t)(st == ORC_INVALID ? 1 : 0);
     }
@@ -633,4 +704,8 @@ int orc_encode_batch(const uint8_t *in, const uint64_t *in_off, uint64_t n, uint
 int orc_decode_batch(const uint8_t *in, const uint64_t *in_off, uint64_t n, uint8_t *out,
                      const uint64_t *out_off, uint32_t *out_len, uint8_t *status, int nthreads) {
   return orc_run(2, in, in_off, n, out, out_off, out_len, status, nthreads);
+}
+int orc_decode_fast_batch(const uint8_t *in, const uint64_t *in_off, uint64_t n, uint8_t *out,
+                          const uint64_t *out_off, uint32_t *out_len, uint8_t *status, int nthreads) {
+  return orc_run(3, in, in_off, n, out, out_off, out_len, status, nthreads);
 }

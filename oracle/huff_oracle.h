@@ -51,6 +51,10 @@ int orc_encode_batch(const uint8_t *in, const uint64_t *in_off, uint64_t n, uint
                      const uint64_t *out_off, int nthreads);
 int orc_decode_batch(const uint8_t *in, const uint64_t *in_off, uint64_t n, uint8_t *out,
                      const uint64_t *out_off, uint32_t *out_len, uint8_t *status, int nthreads);
+/* Table-driven decode with orc_huff_decode's results (CPU baseline only). */
+int orc_huff_decode_fast(const uint8_t *in, size_t len, uint8_t *out, size_t cap, size_t *out_len);
+int orc_decode_fast_batch(const uint8_t *in, const uint64_t *in_off, uint64_t n, uint8_t *out,
+                          const uint64_t *out_off, uint32_t *out_len, uint8_t *status, int nthreads);
 
 #ifdef __cplusplus
 }

@@ -63,6 +63,8 @@ def lib():
         L.orc_encode_len_batch.argtypes = [u8p, u64p, C.c_uint64, u32p, C.c_int]
         L.orc_encode_batch.argtypes = [u8p, u64p, C.c_uint64, u8p, u64p, C.c_int]
         L.orc_decode_batch.argtypes = [u8p, u64p, C.c_uint64, u8p, u64p, u32p, u8p, C.c_int]
+        L.orc_decode_fast_batch.argtypes = [u8p, u64p, C.c_uint64, u8p, u64p, u32p, u8p, C.c_int]
+        L.orc_huff_decode_fast.argtypes = [u8p, sz, u8p, sz, szp]
         _lib = L
     return _lib
 
@@ -232,12 +234,14 @@ def encode_batch(data: np.ndarray, off: np.ndarray, out_off: np.ndarray, nthread
     return out[: int(out_off[-1])]
 
 
-def decode_batch(enc: np.ndarray, off: np.ndarray, cap_off: np.ndarray, nthreads: int = 1):
+def decode_batch(enc: np.ndarray, off: np.ndarray, cap_off: np.ndarray, nthreads: int = 1, fast: bool = False):
+    """Restated Go decode per literal (fast=True: the table-driven decoder,
+    same results; a CPU baseline, not a checker)."""
     n = len(off) - 1
     out = np.zeros(max(int(cap_off[-1]), 1), dtype=np.uint8)
     out_len = np.zeros(n, dtype=np.uint32)
     status = np.zeros(n, dtype=np.uint8)
-    lib().orc_decode_batch(_ptr(enc, C.c_uint8), _ptr(off, C.c_uint64), n, _ptr(out, C.c_uint8),
+    (lib().orc_decode_fast_batch if fast else lib().orc_decode_batch)(_ptr(enc, C.c_uint8), _ptr(off, C.c_uint64), n, _ptr(out, C.c_uint8),
                            _ptr(cap_off, C.c_uint64), _ptr(out_len, C.c_uint32), _ptr(status, C.c_uint8),
                            nthreads)
     return out, out_len, status

@@ -105,3 +105,13 @@ def test_two_rank_gloo_shard_decode_gather():
     assert ok and bad == 0
     assert tmax == 2.0  # max over ranks
     assert ranges[0][0] == 0 and ranges[0][1] == ranges[1][0] and ranges[1][1] == 3000
+
+
+def test_plan_shards_device_matches_host():
+    """bench.py's config-4 split (shard.plan_shards_device, on the device's
+    offsets) equals the host planner."""
+    b = workloads.make_batch(20000, "zipf", "hdr", workloads.SEED_ZIPF)
+    off_t = torch.from_numpy(b.off.view(np.int64).copy())
+    for parts in (1, 2, 3, 8):
+        assert shard.plan_shards_device(off_t, parts) == shard.plan_shards(b.off, parts)
+    assert shard.plan_shards_device(torch.zeros(1, dtype=torch.int64), 4) == [(0, 0)] * 4

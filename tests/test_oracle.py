@@ -197,3 +197,48 @@ def test_workload_labels():
     assert workloads.count_label(1 << 16) == "64K" and workloads.count_label(1000) == "1000"
     assert workloads.config4(1 << 12).name.startswith("config4-4Kx")
     assert workloads.config5(64).name.startswith("config5-64x")
+
+
+def test_table_driven_decoder_matches_restated(oracle_mod):
+    """The table-driven CPU decoder (the honest CPU baseline beside the
+    restated Go loop) gives the restated loop's results: valid
+    literals, 0xff-heavy garbage (INVALID, partial codes) and truncating
+    output regions."""
+    import numpy as np
+
+    rng = np.random.default_rng(3)
+    lits = [bytes(rng.integers(0, 256, rng.integers(0, 60)).astype(np.uint8)) for _ in range(3000)]
+    encs = [oracle_mod.encode(x) for x in lits]
+    lens = rng.integers(0, 40, size=3000)
+    garb = [bytes(np.where(rng.random(k) < 0.5, 0xFF, rng.integers(0, 256, k)).astype(np.uint8)) for k in lens]
+    allb = encs + garb
+    off = np.zeros(len(allb) + 1, dtype=np.uint64)
+    off[1:] = np.cumsum([len(x) for x in allb])
+    data = np.frombuffer(b"".join(allb), dtype=np.uint8).copy()
+    for shrink in (0, 3):  # full capacities, then regions 3 bytes short
+        caps = np.maximum(np.diff(off) * np.uint64(8) // np.uint64(5), np.uint64(shrink)) - np.uint64(shrink)
+        cap = np.zeros(len(off), dtype=np.uint64)
+        cap[1:] = np.cumsum(caps)
+        o1, l1, s1 = oracle_mod.decode_batch(data, off, cap, nthreads=4)
+        o2, l2, s2 = oracle_mod.decode_batch(data, off, cap, nthreads=3, fast=True)
+        assert np.array_equal(l1, l2) and np.array_equal(s1, s2) and s1.sum() > 100
+        for i in range(len(allb)):
+            a = int(cap[i])
+            assert o1[a:a + int(l1[i])].tobytes() == o2[a:a + int(l2[i])].tobytes()
+
+
+@pytest.mark.parametrize("kind,dist,lo,hi,seed", [("uniform", "hdr", 8, 56, 0x6D696E6871),
+                                                  ("zipf", "hdr", 8, 56, 0x7A697066),
+                                                  ("fixed", "adv", 128, 128, 0x616476),
+                                                  ("uniform", "print", 0, 64, 5)])
+def test_device_generator_matches_numpy(kind, dist, lo, hi, seed):
+    """workloads.make_batch_device (torch, here on the CPU) is bit-identical to
+    make_batch (numpy): the full-size bench configs are the same batches."""
+    import numpy as np
+
+    from minhq_amd import workloads
+
+    b = workloads.make_batch(3000, kind, dist, seed, lo, hi)
+    data, off = workloads.make_batch_device(3000, kind, dist, seed, lo, hi, device="cpu", chunk=1 << 12)
+    assert np.array_equal(off.numpy().view(np.uint64), b.off)
+    assert np.array_equal(data.numpy(), b.data)

@@ -94,6 +94,43 @@ def timeline_report(fn):
         prev = np.where(a[:, b + 4] > 0, a[:, b + 4], prev)
 
 
+def wg_report(fn):
+    """Summarises the MHQ_DIAG_WG build's stamps (last launch): stager tile
+    timeline and decoder wait/work split, in us from the workgroup's start."""
+    import ctypes
+
+    T, D = 4, 132
+    S = D + 4 * 16
+    buf = (ctypes.c_ulonglong * (1024 * S))()
+    fn(buf, 1024 * S)
+    a = np.frombuffer(buf, dtype=np.uint64).reshape(1024, S).astype(np.int64)
+    a = a[a[:, 0] > 0]
+    t0 = a[:, 0:1]
+    us = lambda x: (x - t0) / 100.0  # noqa: E731
+    print(f"wg: {a.shape[0]} workgroups, tiles/wg mean {a[:, 3].mean() + 1:.1f}; first publish "
+          f"{np.median(us(a[:, 1:2])):.2f} us, stager end {np.median(us(a[:, 2:3])):.2f} us", file=sys.stderr)
+    names = ["stage", "offsets", "published", "freed", "dma-issued", "records", "last-sub-done", "flush-issued"]
+    for k in range(10):
+        b = T + 8 * k
+        ok = a[:, b] > 0
+        if not ok.any():
+            break
+        x = a[ok]
+        cols = []
+        for q, nm in enumerate(names):
+            v = x[:, b + q]
+            good = v > 0
+            cols.append(f"{nm}@{np.median((v[good] - x[good, 0]) / 100.0):.2f}" if good.any() else f"{nm}@-")
+        print(f"  tile {k}: " + " ".join(cols), file=sys.stderr)
+    dec = a[:, D:].reshape(a.shape[0], 16, 4)
+    live = dec[:, :, 3] > 0
+    wait = dec[:, :, 0][live] / 100.0
+    work = dec[:, :, 1][live] / 100.0
+    end = (dec[:, :, 3] - a[:, 0:1])[live] / 100.0
+    print(f"  decoders: wait {wait.mean():.2f} us, decode {work.mean():.2f} us, sub-tiles "
+          f"{dec[:, :, 2][live].mean():.2f}, end p50 {np.median(end):.2f} max {end.max():.2f} us", file=sys.stderr)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--kernel", default="decode", choices=["decode", "encode", "encode_len", "offsets", "layout"])
@@ -185,6 +222,9 @@ def main():
         it, lanes = buf[0] / args.iters, buf[1] / args.iters
         print(f"diag counts per launch: fast-loop wave iterations {it:.4g}, active lanes {lanes:.4g} "
               f"(utilisation {lanes / max(it * 64, 1):.3f}), per literal {lanes / n:.2f} lane-steps", file=sys.stderr)
+    wg = getattr(_lib.load(), "mhq_diag_wg", None)
+    if wg:
+        wg_report(wg)
     tl = getattr(_lib.load(), "mhq_diag_timeline", None)
     if tl:
         timeline_report(tl)
