@@ -375,13 +375,15 @@ __device__ __forceinline__ void dma_chunks(uint32_t *lds, const uint8_t *g, uint
 __device__ __shared__ uint32_t g_diag_k;
 #endif
 
+// The builtin returns int: each half goes through uint32_t, or a low word
+// >= 2^31 would sign-extend over the high one (offsets of 2-4 GiB, 6-8 GiB...).
 __device__ __forceinline__ uint64_t uniform64(uint64_t v) {
-  return (uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)v) |
-         ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32);
+  return (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)v) |
+         ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32);
 }
 __device__ __forceinline__ uint64_t readlane64(uint64_t v, uint32_t l) {
-  return (uint64_t)__builtin_amdgcn_readlane((uint32_t)v, l) |
-         ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(v >> 32), l) << 32);
+  return (uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)v, l) |
+         ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(v >> 32), l) << 32);
 }
 // Lane l gets lane l+1's value (DPP wave_shl:1); lane 63 gets `last`.
 __device__ __forceinline__ uint32_t from_next_lane(uint32_t v, uint32_t last) {

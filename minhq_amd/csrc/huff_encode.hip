@@ -177,9 +177,11 @@ __device__ __forceinline__ uint32_t vzero() {
 
 __device__ __forceinline__ uint64_t vload(const uint64_t *__restrict__ p, uint64_t i) { return p[i + vzero()]; }
 
+// The builtin returns int: each half goes through uint32_t, or a low word
+// >= 2^31 would sign-extend over the high one (offsets of 2-4 GiB, 6-8 GiB...).
 __device__ __forceinline__ uint64_t uniform64(uint64_t v) {
-  return (uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)v) |
-         ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32);
+  return (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)v) |
+         ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32);
 }
 
 struct Next {           // raw loads for the sub-tile that starts at literal `cur`

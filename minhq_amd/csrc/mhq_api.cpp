@@ -237,8 +237,9 @@ int run_chunk(Device *d, Stage &S, const HostJob &j, uint64_t a, uint64_t b) {
   const uint64_t out_bias = j.out_off[a];
   const uint64_t out_bytes = j.out_off[b] - j.out_off[a];
   MHQ_TRY(hipMemcpyAsync(S.out_off.p, j.out_off + a, (m + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, s));
-  // Regions are fully defined on return: unspecified bytes come back as zeros.
-  MHQ_TRY(hipMemsetAsync(S.out.p, 0, out_bytes, s));
+  // No fill of the staging region: bytes past out_len / enc_len are
+  // unspecified (include/mhq_huff.h), and whatever the kernels leave there is
+  // copied back as is.
   uint8_t *dout = (uint8_t *)S.out.p;
   const uint64_t *dout_off = (const uint64_t *)S.out_off.p;
   if (j.op == Op::kEncode) {
