@@ -527,12 +527,12 @@ def pcie_inclusive(codec, batch):
 def main():
     ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--literals", type=int, default=1 << 20)
     ap.add_argument("--rotate-gib", type=float, default=1.0, help="total bytes of rotating buffer copies")
     ap.add_argument("--cpu-seconds", type=float, default=16.0)
-    ap.add_argument("--long-steps", type=int, default=200, help="steps of the extra long_run timing (0: skip)")
+    ap.add_argument("--long-steps", type=int, default=2000, help="steps of the extra long_run timing (0: skip)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-extras", action="store_true")
     ap.add_argument("--no-configs", action="store_true", help="skip the full-size configs 4 and 5")

@@ -43,16 +43,31 @@ hipError_t launch_decode_wg(const DevTables &t, const uint8_t *in, const uint64_
                             uint64_t in_bias, uint64_t n, uint8_t *out, const uint64_t *out_off,
                             uint64_t out_bias, uint32_t *out_len, uint8_t *status, hipStream_t s);
 // out_off[i] = base + sum_{j<i} enc_len[j]; cap_off[i] = base + sum_{j<i} floor(8*enc_len[j]/5)
-// (either output may be null).  Scratch comes from hipMallocAsync on `s`.
+// (either output may be null).  Scratch: offsets_scratch_bytes(n) bytes, or
+// null for a hipMallocAsync on `s`.
+size_t offsets_scratch_bytes(uint64_t n);
 hipError_t launch_offsets(const uint32_t *enc_len, uint64_t n, uint64_t base, uint64_t *out_off,
-                          uint64_t *cap_off, hipStream_t s);
+                          uint64_t *cap_off, hipStream_t s, void *scratch = nullptr);
+// oa[i] = min(sum_{j<i} a[j], lim_a), ob[i] = min(sum_{j<i} b[j], lim_b) in one scan
+// (a, b 16-B aligned); scratch: offsets_pair_scratch_bytes(n) bytes, or null
+// for a hipMallocAsync on s.
+size_t offsets_pair_scratch_bytes(uint64_t n);
+hipError_t launch_offsets_pair(const uint32_t *a, const uint32_t *b, uint64_t n, uint64_t lim_a, uint64_t lim_b,
+                               uint64_t *oa, uint64_t *ob, void *scratch, hipStream_t s);
+// launch_offsets_pair over per-kLenSumBlock (sum a, sum b) pairs its producer
+// wrote to block_sums (offsets_sums_scratch_bytes(n) bytes; no reduce pass).
+hipError_t launch_offsets_pair_sums(const uint32_t *a, const uint32_t *b, uint64_t n, uint64_t *block_sums,
+                                    uint64_t lim_a, uint64_t lim_b, uint64_t *oa, uint64_t *ob, hipStream_t s);
 // cap_off[i] = base + sum_{j<i} floor(8*(in_off[j+1]-in_off[j])/5): decode capacities
 // for a batch whose encoded offsets are known.
 // Batch ReadString / WriteStringRaw (str_frame.hip); see include/mhq_huff.h.
+// read_strings' scratch: read_strings_scratch_bytes(n, blk_len) bytes, or null
+// for one hipMallocAsync of them on s.
+size_t read_strings_scratch_bytes(uint64_t n, uint64_t blk_len);
 hipError_t launch_read_strings(const DevTables &t, const uint8_t *blk, uint64_t blk_len, const uint64_t *pos,
                                const uint64_t *limit, const uint8_t *prefix, uint64_t n, uint8_t *out,
                                uint64_t out_cap, uint64_t *out_off, uint32_t *out_len, uint8_t *status,
-                               uint64_t *next, hipStream_t s);
+                               uint64_t *next, hipStream_t s, void *scratch = nullptr);
 hipError_t launch_write_strings(const DevTables &t, const uint8_t *in, const uint64_t *in_off, uint64_t n,
                                 const uint8_t *prefix, const uint8_t *lead, uint32_t choice, uint8_t *out,
                                 uint64_t out_cap, uint64_t *out_off, uint8_t *status, hipStream_t s);

@@ -91,6 +91,27 @@ struct CapVal {  // in_off -> decode capacity floor(8*len/5)
   }
 };
 
+struct PairVal {  // two independent u32 lengths -> two offset arrays
+  const uint32_t *a, *b;  // 16-B aligned
+  uint64_t n;
+  __device__ inline void load(uint64_t i0, uint64_t *x, uint64_t *y) const {
+    if (i0 + kItems <= n) {
+#pragma unroll
+      for (int q = 0; q < kItems / 4; q++) {
+        const u32x4 u = ((const u32x4 *)(a + i0))[q], v = ((const u32x4 *)(b + i0))[q];
+        x[4 * q] = u.x; x[4 * q + 1] = u.y; x[4 * q + 2] = u.z; x[4 * q + 3] = u.w;
+        y[4 * q] = v.x; y[4 * q + 1] = v.y; y[4 * q + 2] = v.z; y[4 * q + 3] = v.w;
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < kItems; k++) {
+        x[k] = i0 + k < n ? a[i0 + k] : 0u;
+        y[k] = i0 + k < n ? b[i0 + k] : 0u;
+      }
+    }
+  }
+};
+
 __device__ inline uint64_t wave_sum(uint64_t x) {
 #pragma unroll
   for (int d = 1; d < kWave; d <<= 1) x += __shfl_xor(x, d);
@@ -190,7 +211,8 @@ __global__ __launch_bounds__(kScanBlock) void scan_sums_kernel(uint64_t *sums, u
 template <class F>
 __global__ __launch_bounds__(kScanBlock) void scan_apply_kernel(F f, uint64_t n, const uint64_t *sums,
                                                                  const uint64_t *sup, uint32_t g, uint64_t base,
-                                                                 uint64_t *oa, uint64_t *ob) {
+                                                                 uint64_t *oa, uint64_t *ob, uint64_t lim_a = ~0ull,
+                                                                 uint64_t lim_b = ~0ull) {
   __shared__ uint64_t sh[2 * kWaves];
   const int tid = threadIdx.x, lane = tid % kWave, wave = tid / kWave;
   // this chunk's items first: their loads are in flight during the prefix
@@ -227,8 +249,8 @@ __global__ __launch_bounds__(kScanBlock) void scan_apply_kernel(F f, uint64_t n,
   uint64_t xa[kItems], xb[kItems];
 #pragma unroll
   for (int k = 0; k < kItems; k++) {
-    xa[k] = ra;
-    xb[k] = rb;
+    xa[k] = min(ra, lim_a);  // offsets past a buffer's end become the end
+    xb[k] = min(rb, lim_b);
     ra += a[k];
     rb += b[k];
   }
@@ -269,19 +291,28 @@ __global__ __launch_bounds__(kScanBlock) void scan_apply_kernel(F f, uint64_t n,
 // Superblocks over ns pairs (pair ns included).
 inline uint64_t sup_count(uint64_t ns) { return (ns + 1 + kSup - 1) / kSup; }
 
+inline size_t run_scan_bytes(uint64_t n) {
+  const uint64_t nb = (n + 1 + kChunk - 1) / kChunk;
+  return (size_t)(nb + 1 + sup_count(nb)) * 2 * sizeof(uint64_t);
+}
+
+// `scratch`: run_scan_bytes(n) bytes, or null for a hipMallocAsync of them on s.
 template <class F>
-hipError_t run_scan(F f, uint64_t n, uint64_t base, uint64_t *oa, uint64_t *ob, hipStream_t s) {
+hipError_t run_scan(F f, uint64_t n, uint64_t base, uint64_t *oa, uint64_t *ob, hipStream_t s,
+                    void *scratch = nullptr, uint64_t lim_a = ~0ull, uint64_t lim_b = ~0ull) {
   // n+1 outputs; blocks cover indices 0..n inclusive
   const uint64_t nb = (n + 1 + kChunk - 1) / kChunk;
   const uint64_t nsup = sup_count(nb);
-  uint64_t *sums = nullptr;
-  hipError_t e = hipMallocAsync((void **)&sums, (nb + 1 + nsup) * 2 * sizeof(uint64_t), s);
-  if (e != hipSuccess) return e;
+  uint64_t *sums = (uint64_t *)scratch;
+  hipError_t e = hipSuccess;
+  if (!sums && (e = hipMallocAsync((void **)&sums, run_scan_bytes(n), s)) != hipSuccess) return e;
   uint64_t *sup = sums + 2 * (nb + 1);
   scan_reduce_kernel<F><<<dim3((unsigned)nb), dim3(kScanBlock), 0, s>>>(f, n, sums);
   scan_sums_kernel<<<dim3((unsigned)nsup), dim3(kScanBlock), 0, s>>>(sums, nb, sup);
-  scan_apply_kernel<F><<<dim3((unsigned)nb), dim3(kScanBlock), 0, s>>>(f, n, sums, sup, 1u, base, oa, ob);
+  scan_apply_kernel<F><<<dim3((unsigned)nb), dim3(kScanBlock), 0, s>>>(f, n, sums, sup, 1u, base, oa, ob, lim_a,
+                                                                        lim_b);
   e = hipGetLastError();
+  if (scratch) return e;
   hipError_t e2 = hipFreeAsync(sums, s);
   return e != hipSuccess ? e : e2;
 }
@@ -293,9 +324,11 @@ size_t offsets_sums_scratch_bytes(uint64_t n) {
   return (size_t)(ns + 1 + sup_count(ns)) * 2 * sizeof(uint64_t);
 }
 
+size_t offsets_scratch_bytes(uint64_t n) { return run_scan_bytes(n); }
+
 hipError_t launch_offsets(const uint32_t *enc_len, uint64_t n, uint64_t base, uint64_t *out_off,
-                          uint64_t *cap_off, hipStream_t s) {
-  return run_scan(LenVal{enc_len, n}, n, base, out_off, cap_off, s);
+                          uint64_t *cap_off, hipStream_t s, void *scratch) {
+  return run_scan(LenVal{enc_len, n}, n, base, out_off, cap_off, s, scratch);
 }
 
 hipError_t launch_offsets_sums(const uint32_t *enc_len, uint64_t n, uint64_t *block_sums, uint64_t base,
@@ -310,6 +343,25 @@ hipError_t launch_offsets_sums(const uint32_t *enc_len, uint64_t n, uint64_t *bl
   scan_apply_kernel<LenVal><<<dim3((unsigned)nb), dim3(kScanBlock), 0, s>>>(
       LenVal{enc_len, n}, n, block_sums, sup, (uint32_t)(kChunk / kLenSumBlock), base, out_off, cap_off);
   return hipGetLastError();
+}
+
+size_t offsets_pair_scratch_bytes(uint64_t n) { return run_scan_bytes(n); }
+
+hipError_t launch_offsets_pair_sums(const uint32_t *a, const uint32_t *b, uint64_t n, uint64_t *block_sums,
+                                    uint64_t lim_a, uint64_t lim_b, uint64_t *oa, uint64_t *ob, hipStream_t s) {
+  const uint64_t nb = (n + 1 + kChunk - 1) / kChunk;
+  const uint64_t ns = (n + kLenSumBlock - 1) / kLenSumBlock;
+  const uint64_t nsup = sup_count(ns);
+  uint64_t *sup = block_sums + 2 * (ns + 1);
+  scan_sums_kernel<<<dim3((unsigned)nsup), dim3(kScanBlock), 0, s>>>(block_sums, ns, sup);
+  scan_apply_kernel<PairVal><<<dim3((unsigned)nb), dim3(kScanBlock), 0, s>>>(
+      PairVal{a, b, n}, n, block_sums, sup, (uint32_t)(kChunk / kLenSumBlock), 0, oa, ob, lim_a, lim_b);
+  return hipGetLastError();
+}
+
+hipError_t launch_offsets_pair(const uint32_t *a, const uint32_t *b, uint64_t n, uint64_t lim_a, uint64_t lim_b,
+                               uint64_t *oa, uint64_t *ob, void *scratch, hipStream_t s) {
+  return run_scan(PairVal{a, b, n}, n, 0, oa, ob, s, scratch, lim_a, lim_b);
 }
 
 hipError_t launch_capacity(const uint64_t *in_off, uint64_t n, uint64_t base, uint64_t *cap_off,

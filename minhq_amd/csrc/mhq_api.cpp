@@ -412,7 +412,9 @@ int mhq_huff_offsets_dev(mhq_ctx *ctx, int dev, const uint32_t *enc_len, uint64_
   Device *d = device(ctx, dev);
   if (!d || !out_off || (n && !enc_len)) return MHQ_EINVAL;
   MHQ_TRY(hipSetDevice(d->ordinal));
-  return hip_rc(mhq::launch_offsets(enc_len, n, base, out_off, cap_off, (hipStream_t)stream));
+  hipStream_t s = (hipStream_t)stream;
+  void *scratch = stream_scratch(d, s, mhq::offsets_scratch_bytes(n));
+  return hip_rc(mhq::launch_offsets(enc_len, n, base, out_off, cap_off, s, scratch));
 }
 
 int mhq_huff_encode_layout_dev(mhq_ctx *ctx, int dev, const uint8_t *in, const uint64_t *in_off, uint64_t n,
@@ -466,8 +468,11 @@ int mhq_read_strings_dev(mhq_ctx *ctx, int dev, const uint8_t *blk, uint64_t blk
     return MHQ_EINVAL;
   if (out_cap < blk_len / 5 * 8 + (blk_len % 5) * 8 / 5 + 1) return MHQ_EINVAL;
   MHQ_TRY(hipSetDevice(d->ordinal));
+  hipStream_t s = (hipStream_t)stream;
+  // the stream's cached scratch (null: the launcher allocates in stream order)
+  void *scratch = n ? stream_scratch(d, s, mhq::read_strings_scratch_bytes(n, blk_len)) : nullptr;
   return hip_rc(mhq::launch_read_strings(d->tables, blk, blk_len, pos, limit, prefix, n, out, out_cap, out_off,
-                                         out_len, status, next, (hipStream_t)stream));
+                                         out_len, status, next, s, scratch));
 }
 
 int mhq_write_strings_dev(mhq_ctx *ctx, int dev, const uint8_t *in, const uint64_t *in_off, uint64_t n,

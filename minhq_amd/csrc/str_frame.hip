@@ -11,6 +11,7 @@
 // are integer/byte work with one thread per string.
 #include <hip/hip_runtime.h>
 
+#include "huff_common.h"
 #include "huff_kernels.h"
 
 namespace mhq {
@@ -32,11 +33,41 @@ struct ReadScratch {
 
 // Reader.ReadBit + Reader.ReadInt(prefix) at byte pos, bit 7-prefix being the
 // H bit, reading no byte at or past limit (hc/io.go:25-55, 73-81).
-__global__ void read_parse_kernel(const uint8_t *__restrict__ blk, uint64_t blk_len, const uint64_t *__restrict__ pos,
-                                  const uint64_t *__restrict__ limit, const uint8_t *__restrict__ prefix, uint64_t n,
-                                  ReadScratch sc, uint64_t *__restrict__ next) {
+// Each block also writes the (capacity, Huffman size) sums of its kT strings
+// to block_sums: the offsets scan's first pass.
+__device__ __forceinline__ void block_sums2(uint64_t a, uint64_t b, uint64_t *__restrict__ block_sums) {
+  __shared__ uint64_t part[2 * (kT / 64)];
+  const uint32_t lane = threadIdx.x % 64, wave = threadIdx.x / 64;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    a += __shfl_xor(a, d);
+    b += __shfl_xor(b, d);
+  }
+  if (lane == 0) {
+    part[2 * wave] = a;
+    part[2 * wave + 1] = b;
+  }
+  __syncthreads();
+  if (threadIdx.x < 2) {
+    uint64_t v = 0;
+#pragma unroll
+    for (int w = 0; w < kT / 64; w++) v += part[2 * w + threadIdx.x];
+    block_sums[2 * blockIdx.x + threadIdx.x] = v;
+  }
+}
+
+__global__ __launch_bounds__(kT) void read_parse_kernel(const uint8_t *__restrict__ blk, uint64_t blk_len,
+                                                        const uint64_t *__restrict__ pos,
+                                                        const uint64_t *__restrict__ limit,
+                                                        const uint8_t *__restrict__ prefix, uint64_t n,
+                                                        ReadScratch sc, uint64_t *__restrict__ next,
+                                                        uint64_t *__restrict__ block_sums) {
+  static_assert(kT == kLenSumBlock, "block sums per kLenSumBlock strings");
   const uint64_t i = (uint64_t)blockIdx.x * kT + threadIdx.x;
-  if (i >= n) return;
+  if (i >= n) {
+    block_sums2(0, 0, block_sums);
+    return;
+  }
   // a limit past the block is the block's end: no byte past blk_len is read
   const uint64_t p0 = pos[i], lim = min(limit[i], blk_len);
   const uint32_t pf = prefix[i];
@@ -75,26 +106,99 @@ __global__ void read_parse_kernel(const uint8_t *__restrict__ blk, uint64_t blk_
   sc.take[i] = take;
   sc.declared[i] = kind == 2 ? 0 : v;
   sc.kind[i] = kind;
-  sc.cap[i] = kind == 1 ? (uint32_t)(take * 8 / 5) : (uint32_t)take;
-  sc.hsz[i] = kind == 1 ? (uint32_t)take : 0u;
+  const uint32_t cap = kind == 1 ? (uint32_t)(take * 8 / 5) : (uint32_t)take, hsz = kind == 1 ? (uint32_t)take : 0u;
+  sc.cap[i] = cap;
+  sc.hsz[i] = hsz;
   next[i] = kind == 2 ? p0 : start + take;
+  block_sums2(cap, hsz, block_sums);
 }
 
-// Offsets past a buffer's end become the end, so regions beyond it are empty.
-__global__ void clamp_offsets_kernel(uint64_t *__restrict__ off, uint64_t n1, uint64_t limit) {
-  const uint64_t i = (uint64_t)blockIdx.x * kT + threadIdx.x;
-  if (i < n1 && off[i] > limit) off[i] = limit;
+// len bytes from src to dst, any alignments, by one thread: the 0-3 bytes up
+// to dst's first dword boundary and the 0-3 after its last whole dword go as
+// bytes (neighbouring bytes untouched), the middle as dword stores of source
+// dwords realigned with v_alignbyte.  Every load of a 64-byte block is issued
+// before its first store (no load-store round trip per word).  A source dword
+// read holds at least one byte of [src, src + len): inside any 4-B aligned
+// allocation.
+__device__ __forceinline__ void copy_bytes(uint8_t *__restrict__ dst, const uint8_t *__restrict__ src,
+                                           uint64_t len) {
+  const uint32_t h = (uint32_t)min((uint64_t)((0u - (uint32_t)(uintptr_t)dst) & 3u), len);
+  const uint64_t body = (len - h) & ~(uint64_t)3;
+  const uint32_t t = (uint32_t)(len - h) & 3u;
+  uint32_t hb[3], tb[3];
+#pragma unroll
+  for (uint32_t k = 0; k < 3; k++) {
+    hb[k] = k < h ? src[k] : 0u;
+    tb[k] = k < t ? src[h + body + k] : 0u;
+  }
+  const uint8_t *s1 = src + h;
+  uint32_t *d4 = (uint32_t *)(dst + h);
+  const uint32_t r = (uint32_t)(uintptr_t)s1 & 3u;
+  const uint32_t *w = (const uint32_t *)(s1 - r);
+  const uint64_t nw = body >> 2;
+  for (uint64_t q0 = 0; q0 < nw; q0 += 16) {
+    const uint32_t nq = (uint32_t)min(nw - q0, (uint64_t)16);
+    const uint32_t nload = nq + (r != 0u);
+    uint32_t x[17];
+#pragma unroll
+    for (uint32_t j = 0; j < 17; j++) x[j] = j < nload ? w[q0 + j] : 0u;
+#pragma unroll
+    for (uint32_t j = 0; j < 16; j++)
+      if (j < nq) d4[q0 + j] = __builtin_amdgcn_alignbyte(x[j + 1], x[j], r);
+  }
+#pragma unroll
+  for (uint32_t k = 0; k < 3; k++) {
+    if (k < h) dst[k] = (uint8_t)hb[k];
+    if (k < t) dst[h + body + k] = (uint8_t)tb[k];
+  }
 }
 
-// Huffman payloads into the packed decode input (hin[hin_off[i]..]).
-__global__ void gather_huff_kernel(const uint8_t *__restrict__ blk, ReadScratch sc, uint64_t n,
-                                   const uint64_t *__restrict__ hin_off, uint8_t *__restrict__ hin) {
-  const uint64_t i = (uint64_t)blockIdx.x * kT + threadIdx.x;
-  if (i >= n || sc.kind[i] != 1) return;
-  const uint64_t len = hin_off[i + 1] - hin_off[i];  // clamped: 0 when past the scratch
-  const uint8_t *src = blk + sc.start[i];
-  uint8_t *dst = hin + hin_off[i];
-  for (uint64_t k = 0; k < len; k++) dst[k] = src[k];
+// Huffman payloads into the packed decode input (hin[hin_off[i]..]), a wave
+// per 64 strings.  Their packed destination is one contiguous range, and in a
+// block of consecutive fields their sources are too (payloads separated by
+// the next field's header octets): when both fit kGatherWin bytes, the wave
+// stages the source span into LDS with aligned 16-B loads, each lane moves
+// its payload inside LDS, and the destination leaves as aligned 16-B stores,
+// so global memory sees whole-wave coalesced accesses instead of 64 lanes'
+// scattered dwords.  Other waves (long, overlapping or out-of-order payloads)
+// copy lane by lane from global memory.
+constexpr uint32_t kGatherWin = 4096;
+constexpr int kGatherWaves = kT / 64;
+
+__global__ __launch_bounds__(kT) void gather_huff_kernel(const uint8_t *__restrict__ blk, ReadScratch sc, uint64_t n,
+                                                         const uint64_t *__restrict__ hin_off,
+                                                         uint8_t *__restrict__ hin) {
+  __shared__ __attribute__((aligned(16))) uint8_t win[kGatherWaves][2][kGatherWin];
+  const uint32_t lane = threadIdx.x % 64, wave = threadIdx.x / 64;
+  const uint64_t s0 = (uint64_t)blockIdx.x * kT + (uint64_t)wave * 64;
+  if (s0 >= n) return;
+  const uint64_t i = s0 + lane;
+  const bool live = i < n && sc.kind[i] == 1;
+  const uint64_t d = live ? hin_off[i] : 0, len = live ? hin_off[i + 1] - d : 0;  // clamped: 0 past the scratch
+  const uint64_t src = live ? sc.start[i] : 0;
+  // the wave's source span and destination range
+  uint64_t lo = len ? src : ~0ull, hi = len ? src + len : 0;
+#pragma unroll
+  for (int k = 1; k < 64; k <<= 1) {
+    lo = min(lo, (uint64_t)__shfl_xor((unsigned long long)lo, k));
+    hi = max(hi, (uint64_t)__shfl_xor((unsigned long long)hi, k));
+  }
+  if (hi == 0) return;  // nothing to move (uniform)
+  const uint64_t d0 = hin_off[s0], d1 = hin_off[min(s0 + 64, n)];
+  const uintptr_t sb = (uintptr_t)(blk + lo) & ~(uintptr_t)15, db = (uintptr_t)(hin + d0) & ~(uintptr_t)15;
+  const uint64_t sspan = (uintptr_t)(blk + hi) - sb, dspan = (uintptr_t)(hin + d1) - db;
+  if (sspan > kGatherWin || dspan > kGatherWin) {
+    if (len) copy_bytes(hin + d, blk + src, len);
+    return;
+  }
+  uint8_t *ws = win[wave][0], *wd = win[wave][1];
+  const uint32_t nck = (uint32_t)((sspan + 15) >> 4);  // aligned chunks holding a byte of the span
+  for (uint32_t c = lane; c < nck; c += 64)
+    *(dev::u32x4 *)(ws + 16u * c) = __builtin_nontemporal_load((const dev::u32x4 *)sb + c);
+  dev::wave_sync();
+  if (len) copy_bytes(wd + ((uintptr_t)(hin + d) - db), ws + ((uintptr_t)(blk + src) - sb), len);
+  dev::wave_sync();
+  dev::store_out((uint8_t *)db, wd, (uint32_t)((uintptr_t)(hin + d0) - db), (uint32_t)dspan, (int)lane);
 }
 
 // Raw payloads into the output (after the decode, which zero-fills the
@@ -127,9 +231,7 @@ __global__ void read_finish_kernel(const uint8_t *__restrict__ blk, ReadScratch 
     if (take == 0 && sc.declared[i] > 0) {
       st = MHQ_STR_EOF;  // the block ended before the payload: io.EOF
     } else {
-      const uint8_t *src = blk + sc.start[i];
-      uint8_t *dst = out + out_off[i];
-      for (uint64_t k = 0; k < take; k++) dst[k] = src[k];
+      copy_bytes(out + out_off[i], blk + sc.start[i], take);
       len = (uint32_t)take;
     }
   }
@@ -389,51 +491,73 @@ hipError_t scratch(T **p, uint64_t count, hipStream_t s) {
 
 }  // namespace
 
+namespace {
+
+// read_strings' scratch, 16-B aligned pieces of one allocation.
+struct ReadLayout {
+  size_t start, take, declared, cap, hsz, kind, hin_off, sums, hin, total;
+  ReadLayout(uint64_t n, uint64_t blk_len) {
+    size_t o = 0;
+    auto take_ = [&](size_t bytes) {
+      const size_t at = o;
+      o += (bytes + 15) & ~(size_t)15;
+      return at;
+    };
+    start = take_(8 * n);
+    take = take_(8 * n);
+    declared = take_(8 * n);
+    cap = take_(4 * n);
+    hsz = take_(4 * n);
+    kind = take_(n);
+    hin_off = take_(8 * (n + 1));
+    sums = take_(offsets_sums_scratch_bytes(n));
+    hin = take_(blk_len + 16);
+    total = o;
+  }
+};
+
+}  // namespace
+
+size_t read_strings_scratch_bytes(uint64_t n, uint64_t blk_len) { return ReadLayout(n, blk_len).total; }
+
+// parse (+ block sums) -> one scan of (capacity, Huffman size) into out_off / hin_off, each
+// clamped to its buffer -> gather of the Huffman payloads -> decode -> finish.
 hipError_t launch_read_strings(const DevTables &t, const uint8_t *blk, uint64_t blk_len, const uint64_t *pos,
                                const uint64_t *limit, const uint8_t *prefix, uint64_t n, uint8_t *out,
                                uint64_t out_cap, uint64_t *out_off, uint32_t *out_len, uint8_t *status,
-                               uint64_t *next, hipStream_t s) {
+                               uint64_t *next, hipStream_t s, void *scratch) {
   if (n == 0) {
     return hipMemsetAsync(out_off, 0, sizeof(uint64_t), s);
   }
-  ReadScratch sc{};
-  uint64_t *hin_off = nullptr;
-  uint8_t *hin = nullptr;
+  const ReadLayout L(n, blk_len);
+  uint8_t *base = (uint8_t *)scratch;
   hipError_t e = hipSuccess;
+  if (!base && (e = hipMallocAsync((void **)&base, L.total, s)) != hipSuccess) return e;
+  ReadScratch sc{(uint64_t *)(base + L.start), (uint64_t *)(base + L.take), (uint64_t *)(base + L.declared),
+                 (uint32_t *)(base + L.cap), (uint32_t *)(base + L.hsz), base + L.kind};
+  uint64_t *hin_off = (uint64_t *)(base + L.hin_off);
+  uint8_t *hin = base + L.hin;
 #define TRY(x)                   \
   do {                           \
     e = (x);                     \
     if (e != hipSuccess) goto done; \
   } while (0)
-  TRY(scratch(&sc.start, n, s));
-  TRY(scratch(&sc.take, n, s));
-  TRY(scratch(&sc.declared, n, s));
-  TRY(scratch(&sc.cap, n, s));
-  TRY(scratch(&sc.hsz, n, s));
-  TRY(scratch(&sc.kind, n, s));
-  TRY(scratch(&hin_off, n + 1, s));
-  TRY(scratch(&hin, blk_len + 16, s));
-  read_parse_kernel<<<blocks(n), kT, 0, s>>>(blk, blk_len, pos, limit, prefix, n, sc, next);
+  read_parse_kernel<<<blocks(n), kT, 0, s>>>(blk, blk_len, pos, limit, prefix, n, sc, next,
+                                             (uint64_t *)(base + L.sums));
   TRY(hipGetLastError());
   // output regions: capacities back to back; the packed Huffman input
-  TRY(launch_offsets(sc.cap, n, 0, out_off, nullptr, s));
-  TRY(launch_offsets(sc.hsz, n, 0, hin_off, nullptr, s));
-  clamp_offsets_kernel<<<blocks(n + 1), kT, 0, s>>>(out_off, n + 1, out_cap);
-  clamp_offsets_kernel<<<blocks(n + 1), kT, 0, s>>>(hin_off, n + 1, blk_len);
+  TRY(launch_offsets_pair_sums(sc.cap, sc.hsz, n, (uint64_t *)(base + L.sums), out_cap, blk_len, out_off, hin_off,
+                               s));
   gather_huff_kernel<<<blocks(n), kT, 0, s>>>(blk, sc, n, hin_off, hin);
   TRY(hipGetLastError());
   TRY(launch_decode(t, hin, hin_off, 0, n, out, out_off, 0, out_len, status, s));
   read_finish_kernel<<<blocks(n), kT, 0, s>>>(blk, sc, n, out_off, hin_off, out, out_len, status);
   TRY(hipGetLastError());
 done:
-  (void)hipFreeAsync(sc.start, s);
-  (void)hipFreeAsync(sc.take, s);
-  (void)hipFreeAsync(sc.declared, s);
-  (void)hipFreeAsync(sc.cap, s);
-  (void)hipFreeAsync(sc.hsz, s);
-  (void)hipFreeAsync(sc.kind, s);
-  (void)hipFreeAsync(hin_off, s);
-  (void)hipFreeAsync(hin, s);
+  if (!scratch) {
+    const hipError_t e2 = hipFreeAsync(base, s);
+    if (e == hipSuccess) e = e2;
+  }
   return e;
 }
 

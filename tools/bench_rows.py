@@ -74,8 +74,22 @@ def main():
     nxt = torch.empty(n, dtype=torch.int64, device=dev)
     ms = timed(lambda: codec.read_strings_dev(t_blk, t_pos, t_lim, t_pf, out, out_off, out_len, st, nxt), 10)
     assert int(out_len.sum().item()) == b.nbytes and int((st != 0).sum().item()) == 0
+    # the bare decode of the same literals (packed encodings, floor(8C/5) regions)
+    d_data = torch.from_numpy(b.data).to(dev)
+    d_off = torch.from_numpy(b.off.view(np.int64)).to(dev)
+    e_len = torch.empty(n, dtype=torch.int32, device=dev)
+    e_off = torch.empty(n + 1, dtype=torch.int64, device=dev)
+    c_off = torch.empty(n + 1, dtype=torch.int64, device=dev)
+    codec.encode_layout_dev(d_data, d_off, e_len, e_off, c_off)
+    torch.cuda.synchronize()
+    enc = torch.empty(int(e_off[-1].item()) + 16, dtype=torch.uint8, device=dev)
+    codec.encode_dev(d_data, d_off, enc, e_off)
+    dout = torch.empty(int(c_off[-1].item()) + 16, dtype=torch.uint8, device=dev)
+    bare = timed(lambda: codec.decode_dev(enc, e_off, dout, c_off, out_len, st), 10)
+    assert int(out_len.sum().item()) == b.nbytes and int((st != 0).sum().item()) == 0
     res["read_strings_dev"] = {"strings": n, "block_bytes": int(len(blk)), "decoded_bytes": int(b.nbytes),
-                               "ms": round(ms, 4), "decoded_gib_s": round(b.nbytes / (ms * 1e-3) / 2**30, 2)}
+                               "ms": round(ms, 4), "decoded_gib_s": round(b.nbytes / (ms * 1e-3) / 2**30, 2),
+                               "bare_decode_ms": round(bare, 4), "ratio_to_bare_decode": round(ms / bare, 3)}
 
     # prefix integers: random values / prefixes framed by the GPU writer
     rng = np.random.default_rng(7)

@@ -4,12 +4,12 @@
 set -o pipefail
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 120 --timeout-method thread > gpurun_out/pytest_ab.log 2>&1
+timeout -k 10 300 python -u -m pytest ${TESTS:-tests/test_gpu_parity.py} -x -q --timeout 120 --timeout-method thread > gpurun_out/pytest_ab.log 2>&1
 rc=$?; tail -3 gpurun_out/pytest_ab.log; [ $rc -eq 0 ] || exit $rc
 for cfg in ${CONFIGS:-northstar config2}; do
   for name in default "$@"; do
     lib=build/var/lib_$name.so; [ "$name" = default ] && lib=minhq_amd/libmhq_huff.so
     printf "%-10s " $name
-    MHQ_LIB_PATH=$lib timeout -k 10 120 python3 tools/kernel_driver.py --kernel decode --config $cfg --iters 30 2>&1 | grep -v amdgpu.ids || exit 1
+    MHQ_LIB_PATH=$lib timeout -k 10 120 python3 tools/kernel_driver.py --kernel ${KERNEL:-decode} --config $cfg --iters 30 2>&1 | grep -v amdgpu.ids || exit 1
   done
 done
