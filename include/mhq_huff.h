@@ -75,7 +75,9 @@ int mhq_huff_encode_len(mhq_ctx *ctx, const uint8_t *in, const uint64_t *in_off,
 
 /* HuffmanCompressor.Write + Pad per literal (hc/huffman.go:23-37): codes
  * MSB-first, final octet padded with 1 bits.  out_off[i+1]-out_off[i] must be
- * at least enc_len[i]; bytes past enc_len[i] in a region are unspecified. */
+ * at least enc_len[i]; bytes past enc_len[i] in a region are unspecified.  An
+ * empty region (out_off[i+1] == out_off[i]) skips literal i: nothing of it is
+ * written (a caller encoding a subset places only that subset). */
 int mhq_huff_encode(mhq_ctx *ctx, const uint8_t *in, const uint64_t *in_off, uint64_t n, uint8_t *out,
                     const uint64_t *out_off);
 

@@ -105,8 +105,9 @@ __device__ __forceinline__ uint32_t long_code(const uint16_t *lut2, uint32_t win
 // the staging slices.  Same decision rules as the staged loop.
 __device__ void decode_literal_global(const uint8_t *src, uint64_t nbytes, uint8_t *dst, uint64_t cap,
                                       const Smem &sm, uint32_t *out_len, uint8_t *status) {
-  const uintptr_t a0 = (uintptr_t)src & ~(uintptr_t)3;
-  const uint32_t *wb = (const uint32_t *)a0;
+  const uint8_t *a8 = src - ((uintptr_t)src & 3u);
+  const uintptr_t a0 = (uintptr_t)a8;
+  const uint32_t *wb = (const uint32_t *)a8;
   const uint64_t bit0 = ((uintptr_t)src & 3u) * 8u;
   const uint64_t endbit = bit0 + nbytes * 8u;
   const uint64_t lastw = nbytes ? ((uintptr_t)(src + nbytes - 1) - a0) >> 2 : 0;
@@ -202,6 +203,35 @@ struct BitBuf {
   }
   __device__ __forceinline__ uint32_t top32() const { return (uint32_t)(bb >> 32); }
   // Takes the bit count from an entry's low byte (the shift uses bits [5:0]).
+  __device__ __forceinline__ void consume(uint32_t e) {
+    bb <<= (e & 63u);
+    p += e & 0xffu;
+  }
+};
+
+// BitBuf over words left in memory byte order (LDS-DMA windows): each word
+// is byte-swapped as it is read.
+struct BitBufS {
+  uint64_t bb;
+  uint32_t p, kb, w;
+  const uint32_t *in_w;
+  __device__ __forceinline__ static uint32_t rd(const uint32_t *q, uint32_t k) { return __builtin_bswap32(q[k]); }
+  __device__ __forceinline__ void init(const uint32_t *words, uint32_t p0) {
+    in_w = words;
+    p = p0;
+    const uint32_t k = p0 >> 5;
+    bb = (((uint64_t)rd(in_w, k) << 32) | rd(in_w, k + 1)) << (p0 & 31u);
+    kb = (k + 2u) * 32u;
+    w = rd(in_w, k + 2u);
+  }
+  __device__ __forceinline__ void refill() {
+    const uint32_t nb = kb - p;
+    const bool need = nb <= 32u;
+    bb |= (uint64_t)(need ? w : 0u) << ((32u - nb) & 63u);
+    kb += need ? 32u : 0u;
+    w = rd(in_w, kb >> 5);
+  }
+  __device__ __forceinline__ uint32_t top32() const { return (uint32_t)(bb >> 32); }
   __device__ __forceinline__ void consume(uint32_t e) {
     bb <<= (e & 63u);
     p += e & 0xffu;
@@ -369,6 +399,9 @@ __device__ unsigned long long g_tl[1024 * 16 * kTlSlots];
 // stored after tile k+1's loads are issued and before tile k decodes, and the
 // decode issues no global memory operation: when tile k+1 starts, everything
 // it waits for was issued a whole decode earlier.
+
+typedef __attribute__((address_space(3))) void lds_void;
+typedef __attribute__((address_space(1))) const void g_void;
 
 struct TileOff {  // raw loads: in_off / out_off of literals s + 2*lane + {0, 1}, and of s + tile
   uint64_t i0, i1, o0, o1, ie, oe;
@@ -583,35 +616,67 @@ static_assert(sizeof(uint32_t) * kLongWords * kWave <= sizeof(uint32_t) * (kWIn 
 
 // Output bytes in registers, stored straight to global memory: `acc` holds
 // the bytes from word ow of the literal's 4-B aligned output base up, `ab`
-// bits of it decided.  A completed word inside the literal's region leaves as
-// a dword store; the first word of a region that starts mid-word is shared
-// with the previous literal's region, so it is kept in `first` and finish()
-// writes its bytes one by one, as it does the decided bytes of the last word.
+// bits of it decided.  Completed words inside the literal's region collect in
+// q0..q3 and leave as one aligned 16-B store per four (a lane's stores are
+// scattered over the wave's literals, so each store instruction touches 64
+// lines: four times fewer of them matters more than their width); words of a
+// 16-B group the region does not own whole leave as dword stores.  The first
+// word of a region that starts mid-word is shared with the previous
+// literal's region, so it is kept in `first` and finish() writes its bytes one
+// by one, as it does the decided bytes of the last word.
 struct OutAccG {
   uint64_t acc;
-  uint32_t ow, ab, owf, first, rs;
-  __device__ __forceinline__ void init(uint32_t optr) {
+  uint32_t ow, ab, owf, first, rs, ga, q0, q1, q2, q3;
+  // optr: the region's start from the 4-B aligned base gout; ga: gout's word
+  // position in its 16-B group ((gout / 4) % 4), so word x sits at word
+  // x + ga of the 16-B grid
+  __device__ __forceinline__ void init(uint32_t optr, uint32_t ga_ = 0) {
+    ga = ga_;
     acc = 0;
     ow = optr >> 2;
     ab = (optr & 3u) * 8u;
     owf = (optr + 3u) >> 2;  // the first word owned whole
     first = 0;
     rs = optr;
+    q0 = q1 = q2 = q3 = 0;
   }
   __device__ __forceinline__ void put(uint32_t syms, uint32_t nbits) {
     acc |= (uint64_t)syms << ab;
     ab += nbits;
   }
+  // the 16-B group of word x is owned whole: all four words at or past owf
+  __device__ __forceinline__ bool grouped(uint32_t x) const { return ((x + ga) & ~3u) >= owf + ga; }
   __device__ __forceinline__ void flush(uint32_t *gout) {
     const bool full = ab >= 32u;
-    if (full && ow >= owf) gout[ow] = (uint32_t)acc;
-    first = (full && ow < owf) ? (uint32_t)acc : first;
+    const uint32_t v = (uint32_t)acc;
+#ifndef MHQ_X_LONG_NOSTORE  // timing experiment only: no output stores from the long path
+    if (full && ow >= owf) {
+      if (!grouped(ow)) {
+        gout[ow] = v;
+      } else {
+        const uint32_t r = (ow + ga) & 3u;
+        q0 = r == 0u ? v : q0;
+        q1 = r == 1u ? v : q1;
+        q2 = r == 2u ? v : q2;
+        q3 = r == 3u ? v : q3;
+        if (r == 3u) *(u32x4 *)(gout + ow - 3u) = u32x4{q0, q1, q2, v};
+      }
+    }
+#endif
+    first = (full && ow < owf) ? v : first;
     acc >>= ab & 32u;
     ow += ab >> 5;
     ab &= 31u;
   }
   __device__ __forceinline__ void finish(uint32_t *gout) {
     flush(gout);
+    // whole words of the last, incomplete 16-B group
+    if (grouped(ow)) {
+      const uint32_t r = (ow + ga) & 3u, g = ow - r;
+      if (r > 0u) gout[g] = q0;
+      if (r > 1u) gout[g + 1u] = q1;
+      if (r > 2u) gout[g + 2u] = q2;
+    }
     uint8_t *g8 = (uint8_t *)gout;
     const uint32_t hi = ab >> 3, lo = ow < owf ? (rs & 3u) : 0u;
     if (ow >= owf && (rs & 3u)) {
@@ -624,9 +689,10 @@ struct OutAccG {
 
 // The checked loop of decode_checked on a window, with the lane's running
 // accumulator (roomy literals only: no buffer-full rule).  Returns the status.
+template <class BB>
 __device__ __forceinline__ uint32_t end_checked_g(const Smem &sm, const uint32_t *win, uint32_t p, uint32_t endbit,
                                                   OutAccG &out, uint32_t *gout) {
-  BitBuf in;
+  BB in;
   in.init(win, p);
   uint32_t bad = 0;
   bool fin = false;
@@ -657,10 +723,14 @@ __device__ __forceinline__ uint32_t end_checked_g(const Smem &sm, const uint32_t
 // probe is resolved at once through LUT2 — long literals are where long
 // codes pile up (config 5 has nothing else), and the fast step would spend a
 // second LUT1 probe finding it again.  Same end rules as fast_step.
-template <class Acc>
-__device__ __forceinline__ void long_step(const Smem &sm, uint32_t *otgt, BitBuf &in, Acc &out, uint32_t endbit,
+template <class Acc, class BB>
+__device__ __forceinline__ void long_step(const Smem &sm, uint32_t *otgt, BB &in, Acc &out, uint32_t endbit,
                                           int &lim, uint32_t &bad) {
-  uint32_t e = sm.lut1[in.top32() >> (32 - kLut1Bits)];
+  // kLongOnes or more leading ones can only start a code longer than LUT1's
+  // reach (or the EOS prefix): straight to LUT2, no LUT1 round trip first.
+  const uint32_t top = in.top32();
+  const bool surely_long = top >= (~0u << (32 - kLongOnes));
+  uint32_t e = surely_long ? 0u : sm.lut1[top >> (32 - kLut1Bits)];
   if (e == 0) {
     uint32_t sym = 0;
     const uint32_t L = long_code(sm.lut2, in.top32(), sym);
@@ -709,9 +779,9 @@ __device__ void decode_tile_long(const Smem &sm, WaveSmem &ws, const uint8_t *__
       } else if (oe - ob < (ie - ib) * 8u / 5u) {  // a truncating region: the exact slow path
         decode_literal_global(in + (ib - in_bias), ie - ib, o, oe - ob, sm, out_len + s + j, status + s + j);
       } else {
-        gout = (uint32_t *)((uintptr_t)o & ~(uintptr_t)3);
+        gout = (uint32_t *)(o - ((uintptr_t)o & 3u));  // pointer arithmetic keeps it global: no flat stores
         ostart = (uint32_t)((uintptr_t)o & 3u);
-        acc.init(ostart);
+        acc.init(ostart, (uint32_t)((uintptr_t)gout >> 2) & 3u);
         rel = 0;
         have = true;
         return;
@@ -722,37 +792,48 @@ __device__ void decode_tile_long(const Smem &sm, WaveSmem &ws, const uint8_t *__
   next_lit();
   while (__ballot(have)) {
     // stage: the 8 aligned chunks from the one holding the lane's bit position
-    uint32_t p = 0, endw = 0;
+    // (the last one holding a byte of the literal at most), by LDS-DMA: wave
+    // instruction k loads the windows of lanes 8k..8k+7, 8 lanes a window, so
+    // each instruction reads 8 whole 128-B runs instead of 16 B of 64 runs;
+    // window bytes stay in memory order (BitBufS swaps on read)
+    uint32_t p = 0, endw = 0, nck = 0;
+    uint64_t src = 0;
     if (have) {
       const uint8_t *a = in + (ib - in_bias) + (rel >> 3);
       const uint32_t delta = (uint32_t)((uintptr_t)a & 15u);
-      const u32x4 *src = (const u32x4 *)(a - delta);
+      const uint8_t *a16 = a - delta;
+      src = (uint64_t)(uintptr_t)a16;
       const uint8_t *last = in + (ie - in_bias) - 1;  // the literal's last byte
-      const uint32_t lastc = (uint32_t)(((uintptr_t)last - (uintptr_t)src) >> 4);
-#pragma unroll
-      for (int k = 0; k < (int)(kLongWords / 4); k++) {
-        u32x4 v = __builtin_nontemporal_load(src + min((uint32_t)k, lastc));  // holds a valid byte
-        v.x = __builtin_bswap32(v.x);
-        v.y = __builtin_bswap32(v.y);
-        v.z = __builtin_bswap32(v.z);
-        v.w = __builtin_bswap32(v.w);
-        *(u32x4 *)(win + 4u * k) = v;
-      }
+      nck = min((uint32_t)(((uintptr_t)last - (uintptr_t)a16) >> 4) + 1u, kLongWords / 4u);
       p = delta * 8u + (uint32_t)(rel & 7u);
       endw = p + (uint32_t)((ie - ib) * 8u - rel);  // the literal's end in window bits (may lie beyond)
     }
+#pragma unroll
+    for (uint32_t k = 0; k < kWave / 8u; k++) {
+      const uint32_t o = 8u * k + (lane >> 3), c = lane & 7u;
+      const uint64_t so = (uint64_t)__shfl((unsigned long long)src, (int)o);
+      const uint32_t no = (uint32_t)__shfl((int)nck, (int)o);
+      if (c < no)  // chunks past the literal's last one stay unloaded: their bits are never consumed
+        __builtin_amdgcn_global_load_lds((g_void *)(uintptr_t)(so + 16u * c), (lds_void *)(ws.in_w + 256u * k), 16, 0,
+                                         0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     wave_sync();
     if (have) {
       const bool ends_here = endw + 64u <= kWinBits;
-      BitBuf bin;
+      BitBufS bin;
       bin.init(win, p);
       uint32_t bad = 0;
       const int lim0 = ends_here ? (int)endw - 24 : (int)kSafe;
       int lim = lim0;
+#ifdef MHQ_X_LONG_NODEC  // timing experiment only: windows staged, nothing decoded
+      if ((int)bin.p <= lim) bin.p = (uint32_t)lim + 1u;
+#else
       while ((int)bin.p <= lim) long_step(sm, gout, bin, acc, endw, lim, bad);
+#endif
       const bool stopped = lim == -1 && lim0 != -1;  // a fast step finished the literal (EOS prefix, long code past the end)
       if (stopped || ends_here) {
-        const uint32_t st = stopped ? bad : end_checked_g(sm, win, bin.p, endw, acc, gout);
+        const uint32_t st = stopped ? bad : end_checked_g<BitBufS>(sm, win, bin.p, endw, acc, gout);
         const uint32_t got = acc.optr() - ostart;
         acc.finish(gout);
         out_len[s + j] = got;

@@ -269,7 +269,9 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu((kT / 64 * M
     if (kEmit && pending) store_out(pd_o, (const uint8_t *)sm.out_w, pd_lo, pd_hi, tid, kT);
     pending = false;
     if (oversized) {
-      if (tid == 0) encode_literal_global<kEmit>(ia, i_nxt - i_cur, oa, sm.code, enc_len + cur);
+      // (an empty output region: the caller skips this literal)
+      if (tid == 0 && (!kEmit || o_nxt != o_cur))
+        encode_literal_global<kEmit>(ia, i_nxt - i_cur, oa, sm.code, enc_len + cur);
     } else {
       const uint32_t out_bytes = kEmit ? sm.rec[m] >> 16 : 0u;
       if (kEmit) {
@@ -298,7 +300,10 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu((kT / 64 * M
 #endif
         const uint32_t lit = sm.order[tid];
         const uint32_t r0 = sm.rec[lit], r1 = sm.rec[lit + 1];
-        const uint32_t bits = encode_one<kEmit>(sm, r0 & 0xffffu, r1 & 0xffffu, r0 >> 16);
+        // an empty output region: the caller skips this literal (mhq_huff.h)
+        const uint32_t bits = (!kEmit || (r1 >> 16) != (r0 >> 16))
+                                  ? encode_one<kEmit>(sm, r0 & 0xffffu, r1 & 0xffffu, r0 >> 16)
+                                  : 0u;
         if (!kEmit) enc_len[cur + lit] = (bits + 7u) >> 3;
       }
       __syncthreads();  // in_w free, out_w complete
@@ -418,8 +423,9 @@ __global__ __launch_bounds__(kLenT) void encode_len_kernel(const uint8_t *__rest
     const uint64_t nx = (uint64_t)__shfl_down((unsigned long long)a, 1);  // every lane active: lane 63 is a source
     const uint64_t b = lane < kWave - 1 ? nx : bw;
     const uint64_t aw = uniform64(a);  // lane 0: literal s
-    const uintptr_t base = (uintptr_t)(in + aw) & ~(uintptr_t)15;
-    const u32x4 *src = (const u32x4 *)base;
+    const uint8_t *base8 = in + aw - ((uintptr_t)(in + aw) & 15u);  // pointer arithmetic: global loads, not flat
+    const uintptr_t base = (uintptr_t)base8;
+    const u32x4 *src = (const u32x4 *)base8;
     // aligned chunks holding a byte of [aw, bw): none for an empty range
     const uint64_t nchunk = bw > aw ? ((uintptr_t)(in + bw) - base + 15u) >> 4 : 0u;
     const uint32_t nround = (uint32_t)((nchunk + kWave - 1) / kWave);

@@ -68,9 +68,13 @@ hipError_t launch_read_strings(const DevTables &t, const uint8_t *blk, uint64_t 
                                const uint64_t *limit, const uint8_t *prefix, uint64_t n, uint8_t *out,
                                uint64_t out_cap, uint64_t *out_off, uint32_t *out_len, uint8_t *status,
                                uint64_t *next, hipStream_t s, void *scratch = nullptr);
+// write_strings' scratch: write_strings_scratch_bytes(n, out ? out_cap : 0)
+// bytes, or null for one hipMallocAsync of them on s.
+size_t write_strings_scratch_bytes(uint64_t n, uint64_t out_cap);
 hipError_t launch_write_strings(const DevTables &t, const uint8_t *in, const uint64_t *in_off, uint64_t n,
                                 const uint8_t *prefix, const uint8_t *lead, uint32_t choice, uint8_t *out,
-                                uint64_t out_cap, uint64_t *out_off, uint8_t *status, hipStream_t s);
+                                uint64_t out_cap, uint64_t *out_off, uint8_t *status, hipStream_t s,
+                                void *scratch = nullptr);
 // Batch ReadInt / WriteInt (str_frame.hip); see include/mhq_huff.h.
 hipError_t launch_read_ints(const uint8_t *blk, const uint64_t *pos, const uint64_t *limit, const uint8_t *prefix,
                             uint64_t n, int index, uint64_t *value, uint64_t *next, uint8_t *status, hipStream_t s);

@@ -41,6 +41,12 @@ bool build_tables(Tables *t) {
     t->len[s] = kCodeLen[s];
   }
 
+  // every code with kLongOnes leading ones is longer than LUT1's index
+  for (int s = 0; s < 256; s++) {
+    const uint32_t top = t->code[s] << (32 - t->len[s]);
+    if (top >= (~0u << (32 - kLongOnes)) && t->len[s] <= kLut1Bits) return false;
+  }
+
   // LUT1: up to two symbols from the next 12 bits.
   for (uint32_t idx = 0; idx < (uint32_t)kLut1Size; idx++) {
     int l0 = 0;

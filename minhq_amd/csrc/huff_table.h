@@ -16,6 +16,10 @@ constexpr int kLut1Size = 1 << kLut1Bits;     // 4096 x u32 = 16 KiB of LDS
 constexpr int kLut2SubBits = 5;               // bits after the first 0 of a long code
 constexpr int kLut2Size = 32 << kLut2SubBits; // [leading ones 0..31][5 bits] x u16
 constexpr int kEosOnes = 30;                  // all-ones prefix where EOS would be
+// A code starting with kLongOnes ones is longer than kLut1Bits (the 12-bit
+// codes 0xffa/0xffb have 9): its LUT1 entry is 0, so a decoder may go to LUT2
+// at once.  build_tables() checks it.
+constexpr int kLongOnes = 10;
 
 // LUT1 entry layout (u32), one field per byte so the decode loop can use
 // each field straight from the entry (a 64-bit shift takes its count from

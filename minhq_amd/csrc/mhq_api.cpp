@@ -482,8 +482,10 @@ int mhq_write_strings_dev(mhq_ctx *ctx, int dev, const uint8_t *in, const uint64
   if (!d || !out_off || choice < MHQ_HUFF_AUTO || choice > MHQ_HUFF_NEVER) return MHQ_EINVAL;
   if (n && (!in_off || !prefix || !lead || (out && !status))) return MHQ_EINVAL;
   MHQ_TRY(hipSetDevice(d->ordinal));
+  hipStream_t s = (hipStream_t)stream;
+  void *scratch = n ? stream_scratch(d, s, mhq::write_strings_scratch_bytes(n, out ? out_cap : 0)) : nullptr;
   return hip_rc(mhq::launch_write_strings(d->tables, in, in_off, n, prefix, lead, (uint32_t)choice, out, out_cap,
-                                          out_off, status, (hipStream_t)stream));
+                                          out_off, status, s, scratch));
 }
 
 int mhq_read_ints_dev(mhq_ctx *ctx, int dev, const uint8_t *blk, const uint64_t *pos, const uint64_t *limit,

@@ -185,7 +185,10 @@ __global__ __launch_bounds__(kT) void gather_huff_kernel(const uint8_t *__restri
   }
   if (hi == 0) return;  // nothing to move (uniform)
   const uint64_t d0 = hin_off[s0], d1 = hin_off[min(s0 + 64, n)];
-  const uintptr_t sb = (uintptr_t)(blk + lo) & ~(uintptr_t)15, db = (uintptr_t)(hin + d0) & ~(uintptr_t)15;
+  // aligned bases by pointer arithmetic (global, not flat, memory operations)
+  const uint8_t *sb8 = blk + lo - ((uintptr_t)(blk + lo) & 15u);
+  uint8_t *db8 = hin + d0 - ((uintptr_t)(hin + d0) & 15u);
+  const uintptr_t sb = (uintptr_t)sb8, db = (uintptr_t)db8;
   const uint64_t sspan = (uintptr_t)(blk + hi) - sb, dspan = (uintptr_t)(hin + d1) - db;
   if (sspan > kGatherWin || dspan > kGatherWin) {
     if (len) copy_bytes(hin + d, blk + src, len);
@@ -194,11 +197,11 @@ __global__ __launch_bounds__(kT) void gather_huff_kernel(const uint8_t *__restri
   uint8_t *ws = win[wave][0], *wd = win[wave][1];
   const uint32_t nck = (uint32_t)((sspan + 15) >> 4);  // aligned chunks holding a byte of the span
   for (uint32_t c = lane; c < nck; c += 64)
-    *(dev::u32x4 *)(ws + 16u * c) = __builtin_nontemporal_load((const dev::u32x4 *)sb + c);
+    *(dev::u32x4 *)(ws + 16u * c) = __builtin_nontemporal_load((const dev::u32x4 *)sb8 + c);
   dev::wave_sync();
   if (len) copy_bytes(wd + ((uintptr_t)(hin + d) - db), ws + ((uintptr_t)(blk + src) - sb), len);
   dev::wave_sync();
-  dev::store_out((uint8_t *)db, wd, (uint32_t)((uintptr_t)(hin + d0) - db), (uint32_t)dspan, (int)lane);
+  dev::store_out(db8, wd, (uint32_t)((uintptr_t)(hin + d0) - db), (uint32_t)dspan, (int)lane);
 }
 
 // Raw payloads into the output (after the decode, which zero-fills the
@@ -301,8 +304,19 @@ __global__ void write_frame_kernel(const uint8_t *__restrict__ in, const uint64_
       dst[k++] = (uint8_t)b;
     }
   }
-  for (uint64_t j = 0; j < L; j++) dst[k + j] = src[j];
+  copy_bytes(dst + k, src, L);
   status[i] = MHQ_STR_OK;
+}
+
+// The Huffman payloads the frames will hold: enc_len[i] for a Huffman string
+// whose frame fits the output, 0 otherwise (those are not encoded at all), so
+// the packed encodings total at most out_cap bytes.
+__global__ void write_mask_kernel(const uint32_t *__restrict__ enc_len, const uint8_t *__restrict__ huff,
+                                  const uint64_t *__restrict__ out_off, uint64_t out_cap, uint64_t n,
+                                  uint32_t *__restrict__ mlen) {
+  const uint64_t i = (uint64_t)blockIdx.x * kT + threadIdx.x;
+  if (i >= n) return;
+  mlen[i] = huff[i] && out_off[i + 1] <= out_cap ? enc_len[i] : 0u;
 }
 
 // ---- prefix integers -----------------------------------
@@ -561,44 +575,72 @@ done:
   return e;
 }
 
+namespace {
+
+struct WriteLayout {  // write_strings' scratch, 16-B aligned pieces of one allocation
+  size_t enc_len, frame, mlen, huff, enc_off, sums, enc, total;
+  WriteLayout(uint64_t n, uint64_t out_cap) {
+    size_t o = 0;
+    auto take_ = [&](size_t bytes) {
+      const size_t at = o;
+      o += (bytes + 15) & ~(size_t)15;
+      return at;
+    };
+    enc_len = take_(4 * n);
+    frame = take_(4 * n);
+    mlen = take_(4 * n);
+    huff = take_(n);
+    enc_off = take_(8 * (n + 1));
+    sums = take_(offsets_scratch_bytes(n));
+    enc = take_(out_cap + 16);
+    total = o;
+  }
+};
+
+}  // namespace
+
+size_t write_strings_scratch_bytes(uint64_t n, uint64_t out_cap) { return WriteLayout(n, out_cap).total; }
+
+// encode_len -> choice and frame sizes -> frame offsets -> the Huffman
+// payloads that will be written, packed (at most out_cap bytes: no size has
+// to come back to the host, so no synchronisation) -> encode of just those ->
+// frames.
 hipError_t launch_write_strings(const DevTables &t, const uint8_t *in, const uint64_t *in_off, uint64_t n,
                                 const uint8_t *prefix, const uint8_t *lead, uint32_t choice, uint8_t *out,
-                                uint64_t out_cap, uint64_t *out_off, uint8_t *status, hipStream_t s) {
+                                uint64_t out_cap, uint64_t *out_off, uint8_t *status, hipStream_t s,
+                                void *scratch) {
   if (n == 0) {
     return hipMemsetAsync(out_off, 0, sizeof(uint64_t), s);
   }
-  uint32_t *enc_len = nullptr, *frame = nullptr;
-  uint64_t *enc_off = nullptr;
-  uint8_t *enc = nullptr, *huff = nullptr;
-  uint64_t enc_total = 0, base = 0;
+  // without an output only the offsets are wanted: no room for encodings
+  const WriteLayout L(n, out ? out_cap : 0);
+  uint8_t *base = (uint8_t *)scratch;
   hipError_t e = hipSuccess;
-  TRY(scratch(&enc_len, n, s));
-  TRY(scratch(&frame, n, s));
-  TRY(scratch(&enc_off, n + 1, s));
-  TRY(scratch(&huff, n, s));
+  if (!base && (e = hipMallocAsync((void **)&base, L.total, s)) != hipSuccess) return e;
+  uint32_t *enc_len = (uint32_t *)(base + L.enc_len), *frame = (uint32_t *)(base + L.frame);
+  uint32_t *mlen = (uint32_t *)(base + L.mlen);
+  uint8_t *huff = base + L.huff, *enc = base + L.enc;
+  uint64_t *enc_off = (uint64_t *)(base + L.enc_off);
+  void *sums = base + L.sums;
   TRY(launch_encode_len(t, in, in_off, 0, n, enc_len, s));
-  TRY(hipMemcpyAsync(&base, in_off, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
-  TRY(launch_offsets(enc_len, n, 0, enc_off, nullptr, s));
-  TRY(hipMemcpyAsync(&enc_total, enc_off + n, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
-  TRY(hipStreamSynchronize(s));
-  TRY(scratch(&enc, enc_total + 16, s));
-  TRY(launch_encode(t, in, in_off, 0, n, enc, enc_off, 0, s));
   write_size_kernel<<<blocks(n), kT, 0, s>>>(in_off, enc_len, prefix, choice, n, frame, huff);
   TRY(hipGetLastError());
-  TRY(launch_offsets(frame, n, 0, out_off, nullptr, s));
+  TRY(launch_offsets(frame, n, 0, out_off, nullptr, s, sums));
   if (out) {
+    write_mask_kernel<<<blocks(n), kT, 0, s>>>(enc_len, huff, out_off, out_cap, n, mlen);
+    TRY(hipGetLastError());
+    TRY(launch_offsets(mlen, n, 0, enc_off, nullptr, s, sums));
+    TRY(launch_encode(t, in, in_off, 0, n, enc, enc_off, 0, s));
     write_frame_kernel<<<blocks(n), kT, 0, s>>>(in, in_off, enc, enc_off, prefix, lead, huff, n, out_off, out_cap,
                                                   out, status);
     TRY(hipGetLastError());
   }
 done:
 #undef TRY
-  (void)hipFreeAsync(enc_len, s);
-  (void)hipFreeAsync(frame, s);
-  (void)hipFreeAsync(enc_off, s);
-  (void)hipFreeAsync(enc, s);
-  (void)hipFreeAsync(huff, s);
-  (void)base;
+  if (!scratch) {
+    const hipError_t e2 = hipFreeAsync(base, s);
+    if (e == hipSuccess) e = e2;
+  }
   return e;
 }
 

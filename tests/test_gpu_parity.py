@@ -349,3 +349,33 @@ def test_device_resident_round_trip_adversarial_page_aligned(codec):
     from minhq_amd import workloads
 
     _device_round_trip(codec, workloads.config5(1 << 20))
+
+
+def test_encode_empty_region_skips_literal(codec, oracle_mod):
+    """mhq_huff_encode_dev: a literal whose output region is empty is skipped
+    (nothing written); the others land bit-exactly in their regions.  Covers
+    the staged tiles and a literal larger than the staging slice."""
+    import torch
+
+    from minhq_amd import hc, workloads
+
+    dev = torch.device("cuda", 0)
+    b = workloads.make_batch(5000, "uniform", "hdr", 11, 0, 90)
+    lits = hc.unpack(b.data, b.off)
+    lits[1234] = bytes(range(256)) * 200  # over the staging slice: the global path
+    data, off = hc.pack(lits)
+    rng = np.random.default_rng(4)
+    keep = rng.random(len(lits)) < 0.6
+    keep[1234] = False
+    keep[10] = True
+    lens = np.array([len(oracle_mod.encode(x)) if k else 0 for x, k in zip(lits, keep)], dtype=np.uint64)
+    oo = np.zeros(len(lits) + 1, dtype=np.uint64)
+    oo[1:] = np.cumsum(lens)
+    out = torch.full((int(oo[-1]) + 16,), 0xAB, dtype=torch.uint8, device=dev)
+    codec.encode_dev(torch.from_numpy(data).to(dev), torch.from_numpy(off.view(np.int64)).to(dev), out,
+                     torch.from_numpy(oo.view(np.int64)).to(dev))
+    torch.cuda.synchronize()
+    got = out.cpu().numpy()
+    ref = b"".join(oracle_mod.encode(x) for x, k in zip(lits, keep) if k)
+    assert got[: int(oo[-1])].tobytes() == ref
+    assert (got[int(oo[-1]):] == 0xAB).all()
