@@ -723,7 +723,7 @@ __device__ __forceinline__ uint32_t end_checked_g(const Smem &sm, const uint32_t
 // probe is resolved at once through LUT2 — long literals are where long
 // codes pile up (config 5 has nothing else), and the fast step would spend a
 // second LUT1 probe finding it again.  Same end rules as fast_step.
-template <class Acc, class BB>
+template <class Acc, class BB, bool kFlush = true>
 __device__ __forceinline__ void long_step(const Smem &sm, uint32_t *otgt, BB &in, Acc &out, uint32_t endbit,
                                           int &lim, uint32_t &bad) {
   // kLongOnes or more leading ones can only start a code longer than LUT1's
@@ -745,7 +745,7 @@ __device__ __forceinline__ void long_step(const Smem &sm, uint32_t *otgt, BB &in
   out.put(e >> 16, (e >> 8) & 0xffu);
   in.consume(e);
   in.refill();
-  out.flush(otgt);
+  if (kFlush) out.flush(otgt);
 }
 
 __device__ void decode_tile_long(const Smem &sm, WaveSmem &ws, const uint8_t *__restrict__ in,
@@ -829,6 +829,14 @@ __device__ void decode_tile_long(const Smem &sm, WaveSmem &ws, const uint8_t *__
 #ifdef MHQ_X_LONG_NODEC  // timing experiment only: windows staged, nothing decoded
       if ((int)bin.p <= lim) bin.p = (uint32_t)lim + 1u;
 #else
+      // two probes per flush while two codes (<= 30 bits each) surely fit,
+      // then single ones up to the end test's bound
+      const int lim2 = lim0 - 30;
+      while ((int)bin.p <= lim2 && lim != -1) {
+        long_step<OutAccG, BitBufS, false>(sm, gout, bin, acc, endw, lim, bad);
+        if (lim != -1) long_step<OutAccG, BitBufS, false>(sm, gout, bin, acc, endw, lim, bad);
+        acc.flush(gout);
+      }
       while ((int)bin.p <= lim) long_step(sm, gout, bin, acc, endw, lim, bad);
 #endif
       const bool stopped = lim == -1 && lim0 != -1;  // a fast step finished the literal (EOS prefix, long code past the end)
