@@ -209,14 +209,19 @@ struct BitBuf {
   }
 };
 
-// BitBuf over words left in memory byte order (LDS-DMA windows): each word
-// is byte-swapped as it is read.
+// BitBuf over a long-path window (LDS-DMA): words left in memory byte order
+// (each is byte-swapped as it is read), and the window's 16-B chunks stored
+// XOR-swizzled: chunk c of lane l's window sits in slot c ^ (l % 8), so word k
+// is at k ^ swz with swz = 4 (l % 8).  Lanes walking same-shaped literals read
+// the same k together; unswizzled, all 32 lanes of a half-wave would hit one
+// bank (windows are 32 words apart), swizzled they spread over 8 slots.
 struct BitBufS {
   uint64_t bb;
-  uint32_t p, kb, w;
+  uint32_t p, kb, w, swz;
   const uint32_t *in_w;
-  __device__ __forceinline__ static uint32_t rd(const uint32_t *q, uint32_t k) { return __builtin_bswap32(q[k]); }
-  __device__ __forceinline__ void init(const uint32_t *words, uint32_t p0) {
+  __device__ __forceinline__ uint32_t rd(const uint32_t *q, uint32_t k) const { return __builtin_bswap32(q[k ^ swz]); }
+  __device__ __forceinline__ void init(const uint32_t *words, uint32_t p0, uint32_t swz_) {
+    swz = swz_;
     in_w = words;
     p = p0;
     const uint32_t k = p0 >> 5;
@@ -691,9 +696,9 @@ struct OutAccG {
 // accumulator (roomy literals only: no buffer-full rule).  Returns the status.
 template <class BB>
 __device__ __forceinline__ uint32_t end_checked_g(const Smem &sm, const uint32_t *win, uint32_t p, uint32_t endbit,
-                                                  OutAccG &out, uint32_t *gout) {
+                                                  OutAccG &out, uint32_t *gout, uint32_t swz) {
   BB in;
-  in.init(win, p);
+  in.init(win, p, swz);
   uint32_t bad = 0;
   bool fin = false;
   while (!fin) {
@@ -726,22 +731,26 @@ __device__ __forceinline__ uint32_t end_checked_g(const Smem &sm, const uint32_t
 template <class Acc, class BB, bool kFlush = true>
 __device__ __forceinline__ void long_step(const Smem &sm, uint32_t *otgt, BB &in, Acc &out, uint32_t endbit,
                                           int &lim, uint32_t &bad) {
-  // kLongOnes or more leading ones can only start a code longer than LUT1's
-  // reach (or the EOS prefix): straight to LUT2, no LUT1 round trip first.
+  // Branch free: LUT1 and LUT2 are read together (independent addresses, one
+  // LDS round trip) and the entry is selected after.  kLongOnes or more
+  // leading ones can only start a code longer than LUT1's reach, or the EOS
+  // prefix (c >= 30, LUT2's row clamped to 29 then, its entry unused).
   const uint32_t top = in.top32();
-  const bool surely_long = top >= (~0u << (32 - kLongOnes));
-  uint32_t e = surely_long ? 0u : sm.lut1[top >> (32 - kLut1Bits)];
-  if (e == 0) {
-    uint32_t sym = 0;
-    const uint32_t L = long_code(sm.lut2, in.top32(), sym);
-    const uint32_t left = endbit - in.p;
-    if (L == 0 || L > left) {
-      bad = L == 0 && left > (uint32_t)kEosOnes;  // a 31st bit exists: nil child (hc/huffman.go:111-113)
-      lim = -1;
-    } else {
-      e = L | (8u << 8) | (sym << 16);
-    }
-  }
+  const uint32_t nw = ~top;
+  const uint32_t c = nw ? (uint32_t)__builtin_clz(nw) : 32u;
+  const uint32_t cc = min(c, (uint32_t)kEosOnes - 1u);
+  const uint32_t e2 = sm.lut2[(cc << kLut2SubBits) | ((top << (cc + 1u)) >> (32 - kLut2SubBits))];
+  const uint32_t e1r = sm.lut1[top >> (32 - kLut1Bits)];
+  const uint32_t e1 = c >= (uint32_t)kLongOnes ? 0u : e1r;
+  const uint32_t L = c >= (uint32_t)kEosOnes ? 0u : e2 >> 8;
+  const uint32_t left = endbit - in.p;
+  const bool lng = e1 == 0u;
+  // a long code past the end, or the EOS prefix: the literal ends here, INVALID
+  // when a 31st bit exists (nil child, hc/huffman.go:111-113)
+  const bool stop = lng && (L == 0u || L > left);
+  bad = stop ? (uint32_t)(L == 0u && left > (uint32_t)kEosOnes) : bad;
+  lim = stop ? -1 : lim;
+  const uint32_t e = lng ? (stop ? 0u : (L | (8u << 8) | ((e2 & 0xffu) << 16))) : e1;
   out.put(e >> 16, (e >> 8) & 0xffu);
   in.consume(e);
   in.refill();
@@ -754,6 +763,7 @@ __device__ void decode_tile_long(const Smem &sm, WaveSmem &ws, const uint8_t *__
                                  uint32_t *__restrict__ out_len, uint8_t *__restrict__ status, uint64_t s,
                                  uint32_t cnt, uint32_t lane) {
   uint32_t *win = ws.in_w + lane * kLongWords;  // spans the input and output slices
+  const uint32_t swz = (lane & 7u) << 2;         // BitBufS: the window's chunk swizzle
   constexpr uint32_t kWinBits = kLongWords * 32u;
   constexpr uint32_t kSafe = kWinBits - 96u;  // fast steps stay below: 24 bits + two words of look-ahead
   uint32_t j = lane;
@@ -810,7 +820,8 @@ __device__ void decode_tile_long(const Smem &sm, WaveSmem &ws, const uint8_t *__
     }
 #pragma unroll
     for (uint32_t k = 0; k < kWave / 8u; k++) {
-      const uint32_t o = 8u * k + (lane >> 3), c = lane & 7u;
+      // slot lane % 8 of owner o's window takes chunk (lane % 8) ^ (o % 8)
+      const uint32_t o = 8u * k + (lane >> 3), c = (lane & 7u) ^ (lane >> 3);
       const uint64_t so = (uint64_t)__shfl((unsigned long long)src, (int)o);
       const uint32_t no = (uint32_t)__shfl((int)nck, (int)o);
       if (c < no)  // chunks past the literal's last one stay unloaded: their bits are never consumed
@@ -822,7 +833,7 @@ __device__ void decode_tile_long(const Smem &sm, WaveSmem &ws, const uint8_t *__
     if (have) {
       const bool ends_here = endw + 64u <= kWinBits;
       BitBufS bin;
-      bin.init(win, p);
+      bin.init(win, p, swz);
       uint32_t bad = 0;
       const int lim0 = ends_here ? (int)endw - 24 : (int)kSafe;
       int lim = lim0;
@@ -841,7 +852,7 @@ __device__ void decode_tile_long(const Smem &sm, WaveSmem &ws, const uint8_t *__
 #endif
       const bool stopped = lim == -1 && lim0 != -1;  // a fast step finished the literal (EOS prefix, long code past the end)
       if (stopped || ends_here) {
-        const uint32_t st = stopped ? bad : end_checked_g<BitBufS>(sm, win, bin.p, endw, acc, gout);
+        const uint32_t st = stopped ? bad : end_checked_g<BitBufS>(sm, win, bin.p, endw, acc, gout, swz);
         const uint32_t got = acc.optr() - ostart;
         acc.finish(gout);
         out_len[s + j] = got;
