@@ -358,7 +358,7 @@ __device__ __forceinline__ void len_load_chunks(LenAhead &t, const uint8_t *__re
 }
 
 __device__ __forceinline__ uint32_t len_sum(const LenAhead &t, const uint8_t *__restrict__ in,
-                                            const uint32_t *lens) {
+                                            const uint8_t *lens) {
   const uint64_t a = t.a, b = t.b;
   uint32_t bits = 0;
   const uint64_t c0 = a & ~(uint64_t)15;
@@ -392,7 +392,15 @@ __device__ __forceinline__ uint32_t len_sum(const LenAhead &t, const uint8_t *__
   return bits;
 }
 
-__device__ __forceinline__ uint32_t chunk_bits(const u32x4 &x, const uint32_t *lens, uint32_t q[16]) {
+// Slot of P(x) in a wave's row: lane l's 16 values (4 chunks of 4) go to
+// chunk slots j ^ (l % 4), so the 8 lanes of a ds_write_b128 group spread over
+// the banks (64-B lane stride: linear, lanes l and l+2 collide 4-way).
+// Position kRound (one past the round) stays where it is.
+__device__ __forceinline__ uint32_t prow(uint32_t x) {
+  return x < kRound ? x ^ ((x >> 2) & 0xcu) : x;
+}
+
+__device__ __forceinline__ uint32_t chunk_bits(const u32x4 &x, const uint8_t *lens, uint32_t q[16]) {
   const uint32_t w[4] = {x.x, x.y, x.z, x.w};
   uint32_t t = 0;
 #pragma unroll
@@ -408,7 +416,11 @@ __global__ __launch_bounds__(kLenT) void encode_len_kernel(const uint8_t *__rest
                                                            uint64_t n, uint32_t *__restrict__ enc_len,
                                                            const uint8_t *__restrict__ g_len,
                                                            uint64_t *__restrict__ block_sums) {
-  __shared__ uint32_t lens[256];
+  // code lengths one byte each: byte values b and b+1..b+3 share a dword
+  // (a broadcast), and only b and b+128 share a bank (ds_read_u8 banks by
+  // dword): text lookups are nearly conflict-free, where a u32 table put
+  // 0x21 / 0x41 / 0x61 on one bank
+  __shared__ uint8_t lens[256];
   __shared__ uint32_t pw[kLenT / kWave][kRound + 4];  // P over one round (+ the position after it)
   __shared__ uint64_t part[2 * (kLenT / kWave)];
   const uint32_t lane = threadIdx.x % kWave, wave = threadIdx.x / kWave;
@@ -459,12 +471,12 @@ __global__ __launch_bounds__(kLenT) void encode_len_kernel(const uint8_t *__rest
         const uint32_t pre = carry + wave_incl_scan(tot) - tot;
 #pragma unroll
         for (int j = 0; j < 16; j += 4)
-          *(u32x4 *)(row + 16u * lane + j) = u32x4{pre + q[j], pre + q[j + 1], pre + q[j + 2], pre + q[j + 3]};
+          *(u32x4 *)(row + prow(16u * lane + j)) = u32x4{pre + q[j], pre + q[j + 1], pre + q[j + 2], pre + q[j + 3]};
         if (lane == kWave - 1) row[kRound] = pre + tot;
         wave_sync();
         const uint32_t lo = (r0 + k) * kRound;  // positions [lo, lo + kRound] are in the row
-        if (pa - lo <= kRound) Pa = row[pa - lo];
-        if (pb - lo <= kRound) Pb = row[pb - lo];
+        if (pa - lo <= kRound) Pa = row[prow(pa - lo)];
+        if (pb - lo <= kRound) Pb = row[prow(pb - lo)];
         carry = __builtin_amdgcn_readlane(pre + tot, kWave - 1);
         wave_sync();
       }
