@@ -372,7 +372,7 @@ def test_encode_empty_region_skips_literal(codec, oracle_mod):
     oo = np.zeros(len(lits) + 1, dtype=np.uint64)
     oo[1:] = np.cumsum(lens)
     out = torch.full((int(oo[-1]) + 16,), 0xAB, dtype=torch.uint8, device=dev)
-    codec.encode_dev(torch.from_numpy(data).to(dev), torch.from_numpy(off.view(np.int64)).to(dev), out,
+    codec.encode_dev(torch.from_numpy(data.copy()).to(dev), torch.from_numpy(off.view(np.int64)).to(dev), out,
                      torch.from_numpy(oo.view(np.int64)).to(dev))
     torch.cuda.synchronize()
     got = out.cpu().numpy()
