@@ -73,18 +73,30 @@ def spawn_ranks(n: int) -> int:
     return subprocess.call(cmd, env=env)
 
 
+# Rehearsal knobs for the N > 1 path on a box with fewer GPUs than ranks (the
+# driver's multi-GPU runs set neither): MHQ_BENCH_BACKEND=gloo keeps the
+# barriers and the max-over-ranks on the CPU, MHQ_BENCH_SHARE_GPU=1 maps rank
+# r to GPU r mod (GPUs visible).
+BACKEND = os.environ.get("MHQ_BENCH_BACKEND", "nccl")
+
+
 def dist_setup():
     import torch
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if os.environ.get("MHQ_BENCH_SHARE_GPU") == "1":
+        local %= torch.cuda.device_count()
     torch.cuda.set_device(local)
     pg = None
     if world > 1:
         import torch.distributed as dist
 
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if BACKEND == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(BACKEND)
         pg = dist
     return world, rank, local, pg
 
@@ -101,7 +113,7 @@ def barrier(pg):
 def max_over_ranks(pg, x: float) -> float:
     from minhq_amd import shard
 
-    return shard.max_over_ranks(pg, x, "cuda")
+    return shard.max_over_ranks(pg, x, "cuda" if BACKEND == "nccl" else "cpu")
 
 
 class Slot:
