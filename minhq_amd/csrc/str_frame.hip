@@ -162,7 +162,10 @@ __device__ __forceinline__ void copy_bytes(uint8_t *__restrict__ dst, const uint
 // so global memory sees whole-wave coalesced accesses instead of 64 lanes'
 // scattered dwords.  Other waves (long, overlapping or out-of-order payloads)
 // copy lane by lane from global memory.
-constexpr uint32_t kGatherWin = 4096;
+#ifndef MHQ_GATHER_WIN  // bytes of a wave's source / destination window (LDS: 2 per wave)
+#define MHQ_GATHER_WIN 2048
+#endif
+constexpr uint32_t kGatherWin = MHQ_GATHER_WIN;
 constexpr int kGatherWaves = kT / 64;
 
 __global__ __launch_bounds__(kT) void gather_huff_kernel(const uint8_t *__restrict__ blk, ReadScratch sc, uint64_t n,
