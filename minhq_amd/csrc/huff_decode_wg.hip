@@ -381,10 +381,6 @@ __device__ __forceinline__ uint64_t uniform64(uint64_t v) {
   return (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)v) |
          ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32);
 }
-__device__ __forceinline__ uint64_t readlane64(uint64_t v, uint32_t l) {
-  return (uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)v, l) |
-         ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(v >> 32), l) << 32);
-}
 // Lane l gets lane l+1's value (DPP wave_shl:1); lane 63 gets `last`.
 __device__ __forceinline__ uint32_t from_next_lane(uint32_t v, uint32_t last) {
   return (uint32_t)__builtin_amdgcn_update_dpp((int)last, (int)v, 0x130, 0xf, 0xf, false);

@@ -441,9 +441,16 @@ __global__ __launch_bounds__(kLenT) void encode_len_kernel(const uint8_t *__rest
     // aligned chunks holding a byte of [aw, bw): none for an empty range
     const uint64_t nchunk = bw > aw ? ((uintptr_t)(in + bw) - base + 15u) >> 4 : 0u;
     const uint32_t nround = (uint32_t)((nchunk + kWave - 1) / kWave);
-    // a wave of short literals: one thread per literal is cheaper
+    // With the byte table and the swizzled P rows the cooperative walk beats
+    // one thread per literal even on short literals (config 2: 18.6 -> 15.9
+    // us); the per-thread form (a wave of literals of at most kPre chunks)
+    // stays behind MHQ_LEN_PER_THREAD.
+#ifdef MHQ_LEN_PER_THREAD
     const bool lng = b > a && ((uintptr_t)(in + b) - ((uintptr_t)(in + a) & ~(uintptr_t)15) + 15u) / 16u > kPre;
     if (__ballot(lng) == 0) {
+#else
+    if (false) {
+#endif
       LenAhead t{};
       t.a = a;
       t.b = b;
