@@ -209,6 +209,100 @@ struct BitBuf {
   }
 };
 
+// Ones at the bit positions >= d of a MSB-first word (d clamped to [0, 32]):
+// the part of a staged word that lies at or past a literal's end.
+__device__ __forceinline__ uint32_t ones_past(int32_t d) {
+  const uint32_t c = (uint32_t)min(max(d, 0), 32);
+  return (uint32_t)(0xffffffffull >> c);
+}
+
+// A literal's stream bits in registers with every bit past its end read as a
+// one: `bb` holds bits [p, kb) MSB-aligned (zeros below); staged word kb/32
+// (word index `wi`) is the next to enter; `left` = endbit - p and
+// `rem` = endbit - kb, both signed.  With ones past the end the decode loop
+// needs no end test: a well-formed literal ends in at most 7 padding ones, so
+// the probe at the padding sees >= 30 ones (the EOS prefix) and stops there;
+// a literal whose tail is not all ones decodes a code across its end, which
+// `left < 0` shows (that literal is decoded again by the checked loop).
+struct BitBufM {
+  uint64_t bb;
+  int32_t left, rem;
+  uint32_t wi;
+  const uint32_t *in_w;
+
+  __device__ __forceinline__ void init(const uint32_t *words, uint32_t p0, uint32_t endbit) {
+    in_w = words;
+    const uint32_t k = p0 >> 5;
+    const int32_t e = (int32_t)endbit - (int32_t)(32u * k);
+    const uint32_t w0 = words[k] | ones_past(e), w1 = words[k + 1] | ones_past(e - 32);
+    bb = (((uint64_t)w0 << 32) | w1) << (p0 & 31u);
+    rem = e - 64;
+    wi = k + 2u;
+    left = (int32_t)(endbit - p0);
+  }
+  // The staged word that enters next (read early in a step, used by refill).
+  __device__ __forceinline__ uint32_t next_word() const { return in_w[wi]; }
+  // Tops the buffer up to >= 33 valid bits from `w` = next_word() when it
+  // holds <= 32 (branch free).
+  __device__ __forceinline__ void refill(uint32_t w) {
+    const int32_t nb = left - rem;  // kb - p
+    const bool need = nb <= 32;
+    bb |= (uint64_t)(need ? (w | ones_past(rem)) : 0u) << ((uint32_t)(32 - nb) & 63u);
+    rem -= need ? 32 : 0;
+    wi += need ? 1u : 0u;
+  }
+  __device__ __forceinline__ uint32_t top32() const { return (uint32_t)(bb >> 32); }
+  __device__ __forceinline__ void consume(uint32_t e) {
+    bb <<= (e & 63u);
+    left -= (int32_t)(e & 0xffu);
+  }
+};
+
+// One step of the masked loop (>= 33 valid bits on entry).  The whole window
+// is tested for the EOS prefix first (>= 30 ones: the literal ends here, see
+// BitBufM); a first probe that meets a long code resolves it through LUT2
+// with the whole window and skips the second probe (fewer than 12 valid bits
+// may be left); otherwise two LUT1 probes.  LDS operations complete in issue
+// order, so the previous step's output word (`pend`) and this step's refill
+// word are issued after the first probe: the probe's wait does not include
+// them.  The step's output word becomes the next `pend`, as 0 once a code has
+// crossed the literal's end.  Returns true when the literal is finished:
+// `stop` (EOS prefix at the step's start) or a crossing.
+struct Pend {
+  uint32_t ow, v;
+};
+__device__ __forceinline__ bool masked_step(const Smem &sm, uint32_t *otgt, BitBufM &in, OutAcc &out, Pend &pend,
+                                            bool &stop) {
+  const uint32_t S = in.top32();
+  stop = S >= 0xfffffffcu;
+  uint32_t e = sm.lut1[S >> (32 - kLut1Bits)];
+#if !defined(MHQ_X_NOOR)
+  atomicOr(&otgt[pend.ow], pend.v);
+#endif
+  const uint32_t w = in.next_word();
+  bool lng = false;
+  if (e == 0u && !stop) {  // a code of 13..29 bits
+    uint32_t sym = 0;
+    const uint32_t L = long_code(sm.lut2, S, sym);
+    e = L | (8u << 8) | (sym << 16);
+    lng = true;
+  }
+  out.put(e >> 16, (e >> 8) & 0xffu);
+  in.consume(e);
+  uint32_t e2 = sm.lut1[in.top32() >> (32 - kLut1Bits)];
+  e2 = lng ? 0u : e2;
+  out.put(e2 >> 16, (e2 >> 8) & 0xffu);
+  in.consume(e2);
+  in.refill(w);
+  const bool ok = in.left >= 0;
+  pend.ow = out.ow;
+  pend.v = ok ? (uint32_t)out.acc : 0u;
+  out.acc >>= out.ab & 32u;
+  out.ow += out.ab >> 5;
+  out.ab &= 31u;
+  return stop || !ok;
+}
+
 // BitBuf over a long-path window (LDS-DMA): words left in memory byte order
 // (each is byte-swapped as it is read), and the window's 16-B chunks stored
 // XOR-swizzled: chunk c of lane l's window sits in slot c ^ (l % 8), so word k
@@ -242,83 +336,6 @@ struct BitBufS {
     p += e & 0xffu;
   }
 };
-
-// One fast step at bit p of a literal ending at endbit (p + 24 <= endbit):
-// two LUT1 probes (<= 12 bits each) with no end or room check.  A long code
-// or the EOS prefix has entry 0, which consumes and emits nothing, so the
-// second probe meets it again: one check per step resolves it through LUT2.
-// The EOS prefix (INVALID when a 31st bit follows) and a long code running
-// past the end both finish the literal: `lim` = -1 ends the fast loop and
-// `bad` carries the status.
-template <class Acc>
-__device__ __forceinline__ void fast_step(const Smem &sm, uint32_t *otgt, BitBuf &in, Acc &out, uint32_t endbit,
-                                          int &lim, uint32_t &bad) {
-#ifdef MHQ_X_NOLUT  // timing experiment only (wrong output): every probe is a 2-symbol 10-bit entry
-  uint32_t e = lut1_entry(97, 97, 10, 2) ^ (in.top32() & 0x07070000u);
-#else
-  uint32_t e = sm.lut1[in.top32() >> (32 - kLut1Bits)];
-#endif
-  out.put(e >> 16, (e >> 8) & 0xffu);
-  in.consume(e);
-#ifdef MHQ_X_NOLUT
-  e = lut1_entry(97, 97, 10, 2) ^ (in.top32() & 0x07070000u);
-#else
-  e = sm.lut1[in.top32() >> (32 - kLut1Bits)];
-#endif
-  if (e == 0) {  // a long code or the EOS prefix (the first probe, if it met one, took nothing)
-    in.refill();
-    uint32_t sym = 0;
-    const uint32_t L = long_code(sm.lut2, in.top32(), sym);
-    const uint32_t left = endbit - in.p;
-    if (L == 0 || L > left) {
-      bad = L == 0 && left > (uint32_t)kEosOnes;  // a 31st bit exists: nil child (hc/huffman.go:111-113)
-      lim = -1;
-    } else {
-      e = L | (8u << 8) | (sym << 16);
-    }
-  }
-  out.put(e >> 16, (e >> 8) & 0xffu);
-  in.consume(e);
-  in.refill();
-  out.flush(otgt);
-}
-
-// The last (< 24) bits of a literal whose output region is not truncating:
-// single probes while >= 12 bits are left, then one checked probe, which
-// decodes every code that still fits (three codes need >= 15 bits; a long
-// code cannot fit).  No EOS prefix can be INVALID here (that needs > 30 bits).
-// Returns out_len.
-__device__ __forceinline__ uint32_t decode_end(const Smem &sm, WaveSmem &ws, uint32_t p, uint32_t endbit,
-                                               uint32_t optr, uint32_t ostart) {
-  BitBuf in;
-  in.init(ws.in_w, p);
-  OutAcc out;
-  out.init(optr);
-  bool more = true;
-  while (more && in.p + 12u <= endbit) {
-    uint32_t e = sm.lut1[in.top32() >> (32 - kLut1Bits)];
-    if (e == 0) {
-      uint32_t sym = 0;
-      const uint32_t L = long_code(sm.lut2, in.top32(), sym);
-      more = L != 0 && L <= endbit - in.p;
-      e = more ? (L | (8u << 8) | (sym << 16)) : 0u;
-    }
-    out.put(e >> 16, (e >> 8) & 0xffu);
-    in.consume(e);
-    in.refill();
-    out.flush(ws.out_w);
-  }
-  if (more) {
-    const uint32_t e = sm.lut1[in.top32() >> (32 - kLut1Bits)];
-    const uint32_t left = endbit - in.p;
-    const uint32_t len0 = sm.clen[(e >> 16) & 0xffu];
-    const uint32_t c8 = e == 0 ? 0u : ((e & 0xffu) <= left ? (e >> 8) & 0xffu : (len0 <= left ? 8u : 0u));
-    out.put(__builtin_amdgcn_ubfe(e >> 16, 0, c8), c8);
-  }
-  atomicOr(&ws.out_w[out.ow], (uint32_t)out.acc);
-  if (out.ab > 32u) atomicOr(&ws.out_w[out.ow + 1], (uint32_t)(out.acc >> 32));
-  return out.optr() - ostart;
-}
 
 // The general checked loop (literals with a truncating output region):
 // decodes literal bits [p, endbit) into staging bytes [optr, oend) one probe
@@ -380,12 +397,13 @@ struct LitRef {
 __device__ unsigned long long g_cnt[8];
 #endif
 #ifdef MHQ_DIAG_TIMELINE  // diagnostic build: per-wave timeline (s_memrealtime, 100 MHz)
-constexpr int kTlSlots = 64;  // per wave: [0] start, [63] end, tile j < 20: 1 + 3j + {0 staged, 1 flushed, 2 decoded}
+constexpr int kTlSlots = 64;  // per wave: [0] start, [63] end, tile j < 12: 1 + 5j + {0 loads issued, 1 flushed, 2 sorted, 3 loop done, 4 decoded}
 __device__ unsigned long long g_tl[1024 * 16 * kTlSlots];
 #define TL(slot)                                                                                          \
   do {                                                                                                    \
     const int _s = (slot);                                                                                \
-    if (lane == 0 && _s < kTlSlots) g_tl[(blockIdx.x * 16 + wave) * kTlSlots + _s] = wall_clock64();     \
+    if (threadIdx.x % kWave == 0 && _s < kTlSlots && _s >= 0)                                             \
+      g_tl[(blockIdx.x * 16 + threadIdx.x / kWave) * kTlSlots + _s] = wall_clock64();                     \
   } while (0)
 #else
 #define TL(slot) \
@@ -409,8 +427,11 @@ typedef __attribute__((address_space(3))) void lds_void;
 typedef __attribute__((address_space(1))) const void g_void;
 
 struct TileOff {  // raw loads: in_off / out_off of literals s + 2*lane + {0, 1}, and of s + tile
-  uint64_t i0, i1, o0, o1, ie, oe;
+  uint64_t i0, o0, ie, oe;
+  uint32_t i1, o1;  // only their low words are used (tile-relative offsets): 32-bit loads
 };
+// The low word of a u64 offset.
+__device__ __forceinline__ uint32_t lo32(const uint64_t *a, uint64_t j) { return ((const uint32_t *)a)[2u * j]; }
 
 __device__ __forceinline__ uint32_t vzero() {
   uint32_t z;
@@ -434,10 +455,30 @@ __device__ __forceinline__ void load_off(TileOff &t, const uint64_t *__restrict_
   const uint64_t j0 = min(s + 2u * lane, L1) + z, j1 = min(s + 2u * lane + 1u, L1) + z;
   const uint64_t je = min(s + (uint64_t)tl, L1) + z;
   t.i0 = in_off[j0];
-  t.i1 = in_off[j1];
+  t.i1 = lo32(in_off, j1);
   t.o0 = out_off[j0];
-  t.o1 = out_off[j1];
+  t.o1 = lo32(out_off, j1);
   t.ie = in_off[je];
+  t.oe = out_off[je];
+}
+
+// The two halves of load_off, for the launch's opening.
+__device__ __forceinline__ void load_off_in(TileOff &t, const uint64_t *__restrict__ in_off, uint64_t s, uint64_t L1,
+                                            uint32_t tl, uint32_t lane) {
+  const uint32_t z = vzero();
+  const uint64_t j0 = min(s + 2u * lane, L1) + z, j1 = min(s + 2u * lane + 1u, L1) + z;
+  const uint64_t je = min(s + (uint64_t)tl, L1) + z;
+  t.i0 = in_off[j0];
+  t.i1 = lo32(in_off, j1);
+  t.ie = in_off[je];
+}
+__device__ __forceinline__ void load_off_out(TileOff &t, const uint64_t *__restrict__ out_off, uint64_t s,
+                                             uint64_t L1, uint32_t tl, uint32_t lane) {
+  const uint32_t z = vzero();
+  const uint64_t j0 = min(s + 2u * lane, L1) + z, j1 = min(s + 2u * lane + 1u, L1) + z;
+  const uint64_t je = min(s + (uint64_t)tl, L1) + z;
+  t.o0 = out_off[j0];
+  t.o1 = lo32(out_off, j1);
   t.oe = out_off[je];
 }
 
@@ -448,8 +489,11 @@ struct TileIn {
 // Input chunks [0, kPF*64) from the 16-B aligned start of a tile whose input
 // is [ib, iend) in in_off units (chunk indices clamped; nothing for an empty
 // range, whose aligned chunk may lie past the buffer).
+// `keep` (the opening): the chunk indices come back, for the caller to keep
+// live until the loads have landed (a register that addressed a load still in
+// flight and is then overwritten makes the compiler wait for the load).
 __device__ __forceinline__ void load_in(TileIn &t, const uint8_t *__restrict__ in, uint64_t in_bias, uint64_t ib,
-                                        uint64_t iend, uint32_t lane) {
+                                        uint64_t iend, uint32_t lane, uint32_t *keep = nullptr) {
   const uint8_t *a = in + (ib - in_bias);
   const uint32_t delta = (uint32_t)((uintptr_t)a & 15u);
   const u32x4 *src = (const u32x4 *)(a - delta);
@@ -460,6 +504,7 @@ __device__ __forceinline__ void load_in(TileIn &t, const uint8_t *__restrict__ i
   for (int k = 0; k < kPF; k++) {
     const uint32_t c = min(lane + (uint32_t)kWave * k, chunks - 1u);
     t.v[k] = __builtin_nontemporal_load(src + c);  // aligned, holds a valid byte: never crosses a page
+    if (keep) keep[k] = c;
   }
 }
 
@@ -488,7 +533,7 @@ __device__ __forceinline__ void flush_lens(const WaveSmem &ws, uint64_t s, uint3
 // Decodes the m literals whose boundary records rec[0..m] and input bytes are
 // staged: zero the output region, sort, decode into out_w / len.
 __device__ __forceinline__ void decode_piece(const Smem &sm, WaveSmem &ws, uint32_t m, uint32_t out_bytes,
-                                             uint32_t lane) {
+                                             uint32_t lane, [[maybe_unused]] int tls = -1) {
   for (uint32_t c = lane; c < (out_bytes + 15u) >> 4; c += kWave) *(u32x4 *)(ws.out_w + 4u * c) = u32x4{0u, 0u, 0u, 0u};
   // counting sort by encoded length, longest first
   ws.hist[lane] = 0;
@@ -533,25 +578,25 @@ __device__ __forceinline__ void decode_piece(const Smem &sm, WaveSmem &ws, uint3
   A.load(ws, hasA ? ws.order[lane] : 0u);
   B.load(ws, hasB ? ws.order[2u * kWave - 1u - lane] : 0u);
   const uint32_t ostartA = A.optr, ostartB = B.optr;
+  TL(tls);
+  // Every literal whose region cannot truncate runs the masked loop to its
+  // end (ones past the end: no end test, no separate tail loop); the lane
+  // moves from A to B in place.  A literal with a code across its end (not
+  // well formed) and one whose region truncates take the checked loop.
+  constexpr uint32_t kRedo = 0xffffffffu;
   const bool roomA = hasA && A.roomy(), roomB = hasB && B.roomy();
-  const bool fastA = roomA && A.p + 24u <= A.endbit, fastB = roomB && B.p + 24u <= B.endbit;
-  uint32_t sA = 0, sB = 0;  // 1 | status << 1 once the fast loop has finished the literal
+  uint32_t rA = kRedo, rB = kRedo;
   {
-    const LitRef &C = fastA ? A : B;
-    BitBuf in, inB;  // inB: B's stream, set up once for the in-loop switch
-    in.init(ws.in_w, C.p);
-    inB.init(ws.in_w, B.p);
+    BitBufM in, inB;  // inB: B's stream, set up once for the in-loop switch
+    in.init(ws.in_w, roomA ? A.p : B.p, roomA ? A.endbit : B.endbit);
+    inB.init(ws.in_w, B.p, B.endbit);
     OutAcc out;
-    out.init(C.optr);
-    uint32_t endbit = C.endbit, bad = 0;
-    int lim = (int)endbit - 24;
-    bool onB = !fastA, active = fastA || fastB;
-    // One loop with a single latch: a lane that finishes its first literal's
-    // fast part moves on to its second at once (a loop with a separate
-    // "switch" back edge is restructured into nested loops that run every
-    // lane's first literal to the end before any second one starts).
+    out.init(roomA ? A.optr : B.optr);
+    uint32_t ost = roomA ? ostartA : ostartB;
+    Pend pend{out.ow, 0u};
+    bool onB = !roomA, active = roomA || roomB;
     while (active) {
-#ifdef MHQ_DIAG_COUNT  // diagnostic build: fast-loop wave iterations and active lanes
+#ifdef MHQ_DIAG_COUNT
       {
         const uint64_t mask = __ballot(1);
         if (lane == (uint32_t)__builtin_ctzll(mask)) {
@@ -560,43 +605,25 @@ __device__ __forceinline__ void decode_piece(const Smem &sm, WaveSmem &ws, uint3
         }
       }
 #endif
-      fast_step(sm, ws.out_w, in, out, endbit, lim, bad);
-      if ((int)in.p > lim) {  // this literal's fast part is over (lim = -1: the literal is finished)
-        atomicOr(&ws.out_w[out.ow], (uint32_t)out.acc);  // bits of a completed word not yet written
-        const uint32_t st = lim < 0 ? 1u | (bad << 1) : 0u;
-        if (onB) {
-          B.p = in.p;
-          B.optr = out.optr();
-          sB = st;
-        } else {
-          A.p = in.p;
-          A.optr = out.optr();
-          sA = st;
-        }
-        active = !onB && fastB;
+      bool stop;
+      if (masked_step(sm, ws.out_w, in, out, pend, stop)) {
+        // stop: the EOS prefix at p (INVALID when a 31st bit of the literal follows)
+        const uint32_t r = in.left < 0 ? kRedo : (out.optr() - ost) | ((uint32_t)(in.left > kEosOnes) << 31);
+        atomicOr(&ws.out_w[pend.ow], pend.v);  // the literal's last word
+        pend.v = 0u;
+        rA = onB ? rA : r;
+        rB = onB ? r : rB;
+        active = !onB && roomB;
         in = inB;  // (unused unless active)
         out.init(B.optr);
-        endbit = B.endbit;
-        lim = (int)endbit - 24;
-        bad = 0;
+        ost = ostartB;
         onB = true;
       }
     }
   }
-#ifdef MHQ_X_NOTAIL  // timing experiment only: no literal ends
-  sA |= 1u;
-  sB |= 1u;
-#endif
-  if (hasA) {
-    ws.len[A.lit] = (sA & 1u) ? (A.optr - ostartA) | ((sA >> 1) << 31)
-                    : roomA   ? decode_end(sm, ws, A.p, A.endbit, A.optr, ostartA)
-                              : decode_checked(sm, ws, A.p, A.endbit, A.optr, A.oend);
-  }
-  if (hasB) {
-    ws.len[B.lit] = (sB & 1u) ? (B.optr - ostartB) | ((sB >> 1) << 31)
-                    : roomB   ? decode_end(sm, ws, B.p, B.endbit, B.optr, ostartB)
-                              : decode_checked(sm, ws, B.p, B.endbit, B.optr, B.oend);
-  }
+  TL(tls + 1);
+  if (hasA) ws.len[A.lit] = rA != kRedo ? rA : decode_checked(sm, ws, A.p, A.endbit, A.optr, A.oend);
+  if (hasB) ws.len[B.lit] = rB != kRedo ? rB : decode_checked(sm, ws, B.p, B.endbit, B.optr, B.oend);
   wave_sync();
 }
 
@@ -727,7 +754,7 @@ __device__ __forceinline__ uint32_t end_checked_g(const Smem &sm, const uint32_t
 // One probe of the stream path: a long code (or the EOS prefix) found by the
 // probe is resolved at once through LUT2 — long literals are where long
 // codes pile up (config 5 has nothing else), and the fast step would spend a
-// second LUT1 probe finding it again.  Same end rules as fast_step.
+// second LUT1 probe finding it again.  Same end rules as decode_checked.
 template <class Acc, class BB, bool kFlush = true>
 __device__ __forceinline__ void long_step(const Smem &sm, uint32_t *otgt, BB &in, Acc &out, uint32_t endbit,
                                           int &lim, uint32_t &bad) {
@@ -942,21 +969,40 @@ __global__ __launch_bounds__(kT) void decode_kernel(const uint8_t *__restrict__ 
   // tiles ahead of the one it decodes.
   uint32_t tile = wave, tile2 = tile + kWaves, tile3 = tile + 2 * kWaves;
   TileOff off, off2;
-  load_off(off, in_off, out_off, L0 + (uint64_t)tile * tl0, L1, tl0, lane);
-  load_off(off2, in_off, out_off, L0 + (uint64_t)tile2 * tl0, L1, tl0, lane);
-  for (uint32_t i = tid; i < kLut1Size / 4; i += kT) ((u32x4 *)sm.lut1)[i] = ((const u32x4 *)g_lut1)[i];
-  for (uint32_t i = tid; i < kLut2Size / 8; i += kT) ((u32x4 *)sm.lut2)[i] = ((const u32x4 *)g_lut2)[i];
-  if (tid < 64) ((uint32_t *)sm.clen)[tid] = ((const uint32_t *)g_len)[tid];
-  if (tid == 0) sm.next_tile = 3 * kWaves;
+  // The opening is bound by the bytes every CU loads at once (all of them do),
+  // so loads go in the order they are needed: the batch's boundary offsets
+  // (the tile-length test below), the first tile's input offsets, its input,
+  // then its output offsets, the tables and the second tile's offsets.
+  // (Every wave loads them, as scalar loads, and waits for them only where
+  // they are used: a load under `tid == 0` waited at once.)
+  const uint64_t bnd[4] = {in_off[n], in_off[0], out_off[n], out_off[0]};
+  load_off_in(off, in_off, L0 + (uint64_t)tile * tl0, L1, tl0, lane);
   TileIn tin;
-  load_in(tin, in, in_bias, uniform64(off.i0), uniform64(off.ie), lane);
+  uint32_t keep[kPF] = {};
+  load_in(tin, in, in_bias, uniform64(off.i0), uniform64(off.ie), lane, keep);
+  load_off_out(off, out_off, L0 + (uint64_t)tile * tl0, L1, tl0, lane);
+  static_assert(kLut1Size / 4 <= 2 * kT && kLut2Size / 8 <= kT && kT >= 64, "table copy shape");
+  // (loads and stores from clamped indices, none under a branch: a load
+  // under a branch was waited for inside it, stalling the wave behind its
+  // input loads; threads past a table's end store its last chunk again)
+  const uint32_t x1 = min(tid + (uint32_t)kT, (uint32_t)(kLut1Size / 4) - 1u);
+  const uint32_t x2 = min(tid, (uint32_t)(kLut2Size / 8) - 1u), x3 = tid % 64u;
+  const u32x4 tb0 = ((const u32x4 *)g_lut1)[tid];
+  const u32x4 tb1 = ((const u32x4 *)g_lut1)[x1];
+  const u32x4 tb2 = ((const u32x4 *)g_lut2)[x2];
+  const uint32_t tb3 = ((const uint32_t *)g_len)[x3];
+  load_off(off2, in_off, out_off, L0 + (uint64_t)tile2 * tl0, L1, tl0, lane);
+  ((u32x4 *)sm.lut1)[tid] = tb0;
+  ((u32x4 *)sm.lut1)[x1] = tb1;
+  ((u32x4 *)sm.lut2)[x2] = tb2;
+  ((uint32_t *)sm.clen)[x3] = tb3;
+  if (tid == 0) sm.next_tile = 3 * kWaves;
   // The tile length: the host's tl0 (every wave the same number of tiles)
   // unless the batch's mean literal is too long for tl0 of them to fit the
   // slices, with a 25 % margin; then the most that fit, if that still gives
-  // every lane a literal (longer literals keep tl0 and stream).  The boundary
-  // offsets load beside the tables.
+  // every lane a literal (longer literals keep tl0 and stream).
   if (tid == 0) {
-    const uint64_t nin = in_off[n] - in_off[0], nout = out_off[n] - out_off[0];
+    const uint64_t nin = bnd[0] - bnd[1], nout = bnd[2] - bnd[3];
     const uint64_t ain = (nin + n - 1) / n, aout = (nout + n - 1) / n;
     const uint64_t fit_in = (uint64_t)(kWIn - 16) * 4u / (5u * ain + 8u);
     const uint64_t fit_out = (uint64_t)(kWOut - 16) * 4u / (5u * aout + 8u);
@@ -964,6 +1010,8 @@ __global__ __launch_bounds__(kT) void decode_kernel(const uint8_t *__restrict__ 
     sm.tl = fit >= (uint64_t)kWave && fit < (uint64_t)tl0 ? (uint32_t)fit : tl0;
   }
   __syncthreads();
+#pragma unroll
+  for (int k = 0; k < kPF; k++) asm volatile("" ::"v"(keep[k]));
   const uint32_t tl = __builtin_amdgcn_readfirstlane(sm.tl);
   if (tl != tl0) {  // the loads above used tl0: again with tl
     load_off(off, in_off, out_off, L0 + (uint64_t)tile * tl, L1, tl, lane);
@@ -997,14 +1045,14 @@ __global__ __launch_bounds__(kT) void decode_kernel(const uint8_t *__restrict__ 
       }
       const uint32_t j0 = 2u * lane;
       if (j0 < cnt) ws.rec[j0] = (uint32_t)(off.i0 - ib + idelta) | (uint32_t)(off.o0 - ob + odelta) << 16;
-      if (j0 + 1u < cnt) ws.rec[j0 + 1] = (uint32_t)(off.i1 - ib + idelta) | (uint32_t)(off.o1 - ob + odelta) << 16;
+      if (j0 + 1u < cnt) ws.rec[j0 + 1] = (off.i1 - (uint32_t)ib + idelta) | (off.o1 - (uint32_t)ob + odelta) << 16;
       if (lane == 0) ws.rec[cnt] = (uint32_t)(ie - ib + idelta) | (uint32_t)(oe - ob + odelta) << 16;
     }
     // the next tile's input (its offsets arrived during the previous decode), the offsets of the one after
     load_in(tin, in, in_bias, uniform64(off2.i0), uniform64(off2.ie), lane);
     off = off2;
     load_off(off2, in_off, out_off, L0 + (uint64_t)tile3 * tl, L1, tl, lane);
-    TL(1 + 3 * tl_j);
+    TL(1 + 5 * (int)tl_j);
     // the previous tile's output and lengths leave, then this tile decodes
     if (pd_o) {
       store_out(pd_o, (const uint8_t *)ws.out_w, pd_lo, pd_hi, lane);
@@ -1012,10 +1060,10 @@ __global__ __launch_bounds__(kT) void decode_kernel(const uint8_t *__restrict__ 
     }
     pd_o = nullptr;
     wave_sync();
-    TL(2 + 3 * tl_j);
+    TL(2 + 5 * (int)tl_j);
     if (fits) {
       const uint32_t out_bytes = ws.rec[cnt] >> 16;
-      decode_piece(sm, ws, cnt, out_bytes, lane);
+      decode_piece(sm, ws, cnt, out_bytes, lane, 3 + 5 * (int)tl_j);
       pd_o = oa - odelta;
       pd_lo = odelta;
       pd_hi = out_bytes;
@@ -1033,7 +1081,7 @@ __global__ __launch_bounds__(kT) void decode_kernel(const uint8_t *__restrict__ 
       else
         decode_tile_long(sm, ws, in, in_off, in_bias, out, out_off, out_bias, out_len, status, s, cnt, lane);
     }
-    TL(3 + 3 * tl_j);
+    TL(5 + 5 * (int)tl_j);
     tl_j++;
     tile = tile2;
     tile2 = tile3;
@@ -1073,7 +1121,9 @@ hipError_t launch_decode(const DevTables &t, const uint8_t *in, const uint64_t *
 #endif
   // One workgroup per CU, each a contiguous range of whole wave tiles.  The
   // tile length (<= kTile) is chosen so that every wave gets the same number
-  // of tiles: no wave idles through a last, partial round.
+  // of tiles: no wave idles through a last, partial round.  (A shorter first
+  // round of tiles, 86 + 128 + 128 literals per wave on the north star instead
+  // of 3 x 114, was 1 us slower: the opening does not shorten with its bytes.)
   const uint64_t cus = (uint64_t)dev::device_cus();
   const uint64_t slots = cus * kWaves;
   const uint64_t rounds = (n + slots * kTile - 1) / (slots * kTile) + MHQ_DEC_XROUNDS;
