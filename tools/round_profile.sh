@@ -8,7 +8,7 @@ set -o pipefail
 export TMPDIR=/tmp
 OUT=${1:-gpurun_out/round}
 mkdir -p "$OUT"
-BENCH="bench.py --steps 20 --warmup 5"
+BENCH="bench.py"
 timeout -k 10 600 python3 $BENCH --cpu-seconds 15 > "$OUT/bench.json" 2> "$OUT/bench.err" || { echo "bench failed"; tail "$OUT/bench.err"; exit 1; }
 cat "$OUT/bench.json"
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/stats" -o run -- python3 $BENCH --no-cpu --no-extras \
