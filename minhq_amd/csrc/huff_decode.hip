@@ -378,13 +378,16 @@ __device__ __noinline__ uint32_t decode_checked(const Smem &sm, WaveSmem &ws, ui
 }
 
 // A literal's place in the staged tile.
+// (kGaps: literal l's input ends at ws.len[l], not where literal l + 1
+// starts; see decode_kernel.)
+template <bool kGaps>
 struct LitRef {
   uint32_t lit, p, endbit, optr, oend;
   __device__ __forceinline__ void load(const WaveSmem &ws, uint32_t l) {
     lit = l;
     const uint32_t r0 = ws.rec[l], r1 = ws.rec[l + 1];
     p = (r0 & 0xffffu) * 8u;
-    endbit = (r1 & 0xffffu) * 8u;
+    endbit = (kGaps ? ws.len[l] : (r1 & 0xffffu)) * 8u;
     optr = r0 >> 16;
     oend = r1 >> 16;
   }
@@ -429,6 +432,7 @@ typedef __attribute__((address_space(1))) const void g_void;
 struct TileOff {  // raw loads: in_off / out_off of literals s + 2*lane + {0, 1}, and of s + tile
   uint64_t i0, o0, ie, oe;
   uint32_t i1, o1;  // only their low words are used (tile-relative offsets): 32-bit loads
+  uint32_t e0, e1;  // kGaps: in_end of the two literals (low words)
 };
 // The low word of a u64 offset.
 __device__ __forceinline__ uint32_t lo32(const uint64_t *a, uint64_t j) { return ((const uint32_t *)a)[2u * j]; }
@@ -448,14 +452,19 @@ __device__ __forceinline__ uint64_t uniform64(uint64_t v) {
 
 // Offsets of the tile that starts at literal s (indices clamped to L1, so a
 // tile past the range loads the range end).
+template <bool kGaps>
 __device__ __forceinline__ void load_off(TileOff &t, const uint64_t *__restrict__ in_off,
-                                         const uint64_t *__restrict__ out_off, uint64_t s, uint64_t L1,
-                                         uint32_t tl, uint32_t lane) {
+                                         const uint64_t *__restrict__ in_end, const uint64_t *__restrict__ out_off,
+                                         uint64_t s, uint64_t L1, uint32_t tl, uint32_t lane) {
   const uint32_t z = vzero();  // keeps the loads per-lane vector loads
   const uint64_t j0 = min(s + 2u * lane, L1) + z, j1 = min(s + 2u * lane + 1u, L1) + z;
   const uint64_t je = min(s + (uint64_t)tl, L1) + z;
   t.i0 = in_off[j0];
   t.i1 = lo32(in_off, j1);
+  if (kGaps) {  // (in_end has n entries: indices clamped below L1)
+    t.e0 = lo32(in_end, min(j0, L1 - 1u));
+    t.e1 = lo32(in_end, min(j1, L1 - 1u));
+  }
   t.o0 = out_off[j0];
   t.o1 = lo32(out_off, j1);
   t.ie = in_off[je];
@@ -463,13 +472,19 @@ __device__ __forceinline__ void load_off(TileOff &t, const uint64_t *__restrict_
 }
 
 // The two halves of load_off, for the launch's opening.
-__device__ __forceinline__ void load_off_in(TileOff &t, const uint64_t *__restrict__ in_off, uint64_t s, uint64_t L1,
+template <bool kGaps>
+__device__ __forceinline__ void load_off_in(TileOff &t, const uint64_t *__restrict__ in_off,
+                                            const uint64_t *__restrict__ in_end, uint64_t s, uint64_t L1,
                                             uint32_t tl, uint32_t lane) {
   const uint32_t z = vzero();
   const uint64_t j0 = min(s + 2u * lane, L1) + z, j1 = min(s + 2u * lane + 1u, L1) + z;
   const uint64_t je = min(s + (uint64_t)tl, L1) + z;
   t.i0 = in_off[j0];
   t.i1 = lo32(in_off, j1);
+  if (kGaps) {
+    t.e0 = lo32(in_end, min(j0, L1 - 1u));
+    t.e1 = lo32(in_end, min(j1, L1 - 1u));
+  }
   t.ie = in_off[je];
 }
 __device__ __forceinline__ void load_off_out(TileOff &t, const uint64_t *__restrict__ out_off, uint64_t s,
@@ -532,6 +547,7 @@ __device__ __forceinline__ void flush_lens(const WaveSmem &ws, uint64_t s, uint3
 
 // Decodes the m literals whose boundary records rec[0..m] and input bytes are
 // staged: zero the output region, sort, decode into out_w / len.
+template <bool kGaps>
 __device__ __forceinline__ void decode_piece(const Smem &sm, WaveSmem &ws, uint32_t m, uint32_t out_bytes,
                                              uint32_t lane, [[maybe_unused]] int tls = -1) {
   for (uint32_t c = lane; c < (out_bytes + 15u) >> 4; c += kWave) *(u32x4 *)(ws.out_w + 4u * c) = u32x4{0u, 0u, 0u, 0u};
@@ -545,7 +561,7 @@ __device__ __forceinline__ void decode_piece(const Smem &sm, WaveSmem &ws, uint3
     key[h] = 0;
     rk[h] = 0;
     if (j < m) {
-      const uint32_t bytes = (ws.rec[j + 1] & 0xffffu) - (ws.rec[j] & 0xffffu);
+      const uint32_t bytes = (kGaps ? ws.len[j] : (ws.rec[j + 1] & 0xffffu)) - (ws.rec[j] & 0xffffu);
       const uint32_t bk = bytes < 48u ? bytes : min(48u + ((bytes - 48u) >> 3), (uint32_t)kBuckets - 1u);
       key[h] = (uint32_t)kBuckets - 1u - bk;
       rk[h] = atomicAdd(&ws.hist[key[h]], 1u);
@@ -574,7 +590,7 @@ __device__ __forceinline__ void decode_piece(const Smem &sm, WaveSmem &ws, uint3
   return;
 #endif
   const bool hasA = lane < m, hasB = 2u * kWave - 1u - lane < m;
-  LitRef A, B;
+  LitRef<kGaps> A, B;
   A.load(ws, hasA ? ws.order[lane] : 0u);
   B.load(ws, hasB ? ws.order[2u * kWave - 1u - lane] : 0u);
   const uint32_t ostartA = A.optr, ostartB = B.optr;
@@ -784,8 +800,10 @@ __device__ __forceinline__ void long_step(const Smem &sm, uint32_t *otgt, BB &in
   if (kFlush) out.flush(otgt);
 }
 
+template <bool kGaps>
 __device__ void decode_tile_long(const Smem &sm, WaveSmem &ws, const uint8_t *__restrict__ in,
-                                 const uint64_t *__restrict__ in_off, uint64_t in_bias, uint8_t *__restrict__ out,
+                                 const uint64_t *__restrict__ in_off, const uint64_t *__restrict__ in_end,
+                                 uint64_t in_bias, uint8_t *__restrict__ out,
                                  const uint64_t *__restrict__ out_off, uint64_t out_bias,
                                  uint32_t *__restrict__ out_len, uint8_t *__restrict__ status, uint64_t s,
                                  uint32_t cnt, uint32_t lane) {
@@ -806,7 +824,7 @@ __device__ void decode_tile_long(const Smem &sm, WaveSmem &ws, const uint8_t *__
     have = false;
     while (j < cnt) {
       ib = in_off[s + j];
-      ie = in_off[s + j + 1];
+      ie = kGaps ? in_end[s + j] : in_off[s + j + 1];
       ob = out_off[s + j];
       const uint64_t oe = out_off[s + j + 1];
       uint8_t *o = out + (ob - out_bias);
@@ -938,7 +956,7 @@ __device__ void decode_tile_pieces(const Smem &sm, WaveSmem &ws, const uint8_t *
     const uint32_t in_bytes = ws.rec[m] & 0xffffu, out_bytes = ws.rec[m] >> 16;
     stage_in<true, false>(ws.in_w, kWIn / 4, ia - idelta, in_bytes, lane);
     wave_sync();
-    decode_piece(sm, ws, m, out_bytes, lane);
+    decode_piece<false>(sm, ws, m, out_bytes, lane);
     store_out(oa - odelta, (const uint8_t *)ws.out_w, odelta, out_bytes, lane);
     flush_lens(ws, s + cur, m, out_len, status, lane);
     wave_sync();
@@ -946,7 +964,15 @@ __device__ void decode_tile_pieces(const Smem &sm, WaveSmem &ws, const uint8_t *
   }
 }
 
+// kGaps: literal i is in[in_off[i] .. in_end[i]), in_end[i] <= in_off[i + 1]
+// (the bytes between belong to no literal: the Huffman payloads of a block of
+// framed string fields, read where they lie).  A tile is staged only when its
+// literals are in that order and fit; every other tile streams (decode_tile_long,
+// any order, overlaps included).  The staged tile keeps each literal's end in
+// its len slot until the results overwrite it.
+template <bool kGaps>
 __global__ __launch_bounds__(kT) void decode_kernel(const uint8_t *__restrict__ in, const uint64_t *__restrict__ in_off,
+                                                    const uint64_t *__restrict__ in_end,
                                                     uint64_t in_bias, uint64_t n, uint8_t *__restrict__ out,
                                                     const uint64_t *__restrict__ out_off, uint64_t out_bias,
                                                     uint32_t *__restrict__ out_len, uint8_t *__restrict__ status,
@@ -976,7 +1002,7 @@ __global__ __launch_bounds__(kT) void decode_kernel(const uint8_t *__restrict__ 
   // (Every wave loads them, as scalar loads, and waits for them only where
   // they are used: a load under `tid == 0` waited at once.)
   const uint64_t bnd[4] = {in_off[n], in_off[0], out_off[n], out_off[0]};
-  load_off_in(off, in_off, L0 + (uint64_t)tile * tl0, L1, tl0, lane);
+  load_off_in<kGaps>(off, in_off, in_end, L0 + (uint64_t)tile * tl0, L1, tl0, lane);
   TileIn tin;
   uint32_t keep[kPF] = {};
   load_in(tin, in, in_bias, uniform64(off.i0), uniform64(off.ie), lane, keep);
@@ -991,7 +1017,7 @@ __global__ __launch_bounds__(kT) void decode_kernel(const uint8_t *__restrict__ 
   const u32x4 tb1 = ((const u32x4 *)g_lut1)[x1];
   const u32x4 tb2 = ((const u32x4 *)g_lut2)[x2];
   const uint32_t tb3 = ((const uint32_t *)g_len)[x3];
-  load_off(off2, in_off, out_off, L0 + (uint64_t)tile2 * tl0, L1, tl0, lane);
+  load_off<kGaps>(off2, in_off, in_end, out_off, L0 + (uint64_t)tile2 * tl0, L1, tl0, lane);
   ((u32x4 *)sm.lut1)[tid] = tb0;
   ((u32x4 *)sm.lut1)[x1] = tb1;
   ((u32x4 *)sm.lut2)[x2] = tb2;
@@ -1014,8 +1040,8 @@ __global__ __launch_bounds__(kT) void decode_kernel(const uint8_t *__restrict__ 
   for (int k = 0; k < kPF; k++) asm volatile("" ::"v"(keep[k]));
   const uint32_t tl = __builtin_amdgcn_readfirstlane(sm.tl);
   if (tl != tl0) {  // the loads above used tl0: again with tl
-    load_off(off, in_off, out_off, L0 + (uint64_t)tile * tl, L1, tl, lane);
-    load_off(off2, in_off, out_off, L0 + (uint64_t)tile2 * tl, L1, tl, lane);
+    load_off<kGaps>(off, in_off, in_end, out_off, L0 + (uint64_t)tile * tl, L1, tl, lane);
+    load_off<kGaps>(off2, in_off, in_end, out_off, L0 + (uint64_t)tile2 * tl, L1, tl, lane);
     load_in(tin, in, in_bias, uniform64(off.i0), uniform64(off.ie), lane);
   }
   const uint32_t ntiles = (uint32_t)((L1 - L0 + tl - 1) / tl);
@@ -1032,7 +1058,19 @@ __global__ __launch_bounds__(kT) void decode_kernel(const uint8_t *__restrict__ 
     const uint8_t *ia = in + (ib - in_bias);
     uint8_t *oa = out + (ob - out_bias);
     const uint32_t idelta = (uint32_t)((uintptr_t)ia & 15u), odelta = (uint32_t)((uintptr_t)oa & 15u);
-    const bool fits = (ie - ib) + idelta <= (uint64_t)kWIn && (oe - ob) + odelta <= (uint64_t)kWOut;
+    bool fits = (ie - ib) + idelta <= (uint64_t)kWIn && (oe - ob) + odelta <= (uint64_t)kWOut;
+    uint32_t re0 = 0, re1 = 0;  // kGaps: the two literals' ends in the slice
+    if (kGaps) {  // staged only if start <= end <= next start for every literal of the tile
+      const uint32_t ib32 = (uint32_t)ib - idelta;
+      const uint32_t a = (uint32_t)off.i0 - ib32, c = off.i1 - ib32, rie = (uint32_t)ie - ib32;
+      re0 = off.e0 - ib32;
+      re1 = off.e1 - ib32;
+      const uint32_t nx = (uint32_t)__shfl_down((int)a, 1);  // the next lane's first start
+      const uint32_t j0 = 2u * lane;
+      const bool ok0 = j0 >= cnt || (a <= re0 && re0 <= (j0 + 1u < cnt ? c : rie));
+      const bool ok1 = j0 + 1u >= cnt || (c <= re1 && re1 <= (j0 + 2u < cnt ? nx : rie));
+      fits = fits && __ballot(!(ok0 && ok1)) == 0;
+    }
     // claim the tile three ahead (used when this one is done)
     uint32_t tile4 = 0;
     if (lane == 0) tile4 = atomicAdd(&sm.next_tile, 1u);
@@ -1051,7 +1089,7 @@ __global__ __launch_bounds__(kT) void decode_kernel(const uint8_t *__restrict__ 
     // the next tile's input (its offsets arrived during the previous decode), the offsets of the one after
     load_in(tin, in, in_bias, uniform64(off2.i0), uniform64(off2.ie), lane);
     off = off2;
-    load_off(off2, in_off, out_off, L0 + (uint64_t)tile3 * tl, L1, tl, lane);
+    load_off<kGaps>(off2, in_off, in_end, out_off, L0 + (uint64_t)tile3 * tl, L1, tl, lane);
     TL(1 + 5 * (int)tl_j);
     // the previous tile's output and lengths leave, then this tile decodes
     if (pd_o) {
@@ -1062,8 +1100,14 @@ __global__ __launch_bounds__(kT) void decode_kernel(const uint8_t *__restrict__ 
     wave_sync();
     TL(2 + 5 * (int)tl_j);
     if (fits) {
+      if (kGaps) {  // the ends go in the len slots once the previous tile's lengths have left
+        const uint32_t j0 = 2u * lane;
+        if (j0 < cnt) ws.len[j0] = re0;
+        if (j0 + 1u < cnt) ws.len[j0 + 1] = re1;
+        wave_sync();
+      }
       const uint32_t out_bytes = ws.rec[cnt] >> 16;
-      decode_piece(sm, ws, cnt, out_bytes, lane, 3 + 5 * (int)tl_j);
+      decode_piece<kGaps>(sm, ws, cnt, out_bytes, lane, 3 + 5 * (int)tl_j);
       pd_o = oa - odelta;
       pd_lo = odelta;
       pd_hi = out_bytes;
@@ -1072,14 +1116,16 @@ __global__ __launch_bounds__(kT) void decode_kernel(const uint8_t *__restrict__ 
     } else {
       // a tile a little over the slice (short literals with a few long ones)
       // goes in staged pieces; one of long literals streams through windows
+      // (kGaps: every such tile streams)
 #ifdef MHQ_X_NOLONG  // timing experiment: the piece path for every oversized tile
-      if (true)
+      if (!kGaps)
 #else
-      if ((ie - ib) <= 2u * (uint64_t)kWIn && (oe - ob) <= 2u * (uint64_t)kWOut)
+      if (!kGaps && (ie - ib) <= 2u * (uint64_t)kWIn && (oe - ob) <= 2u * (uint64_t)kWOut)
 #endif
         decode_tile_pieces(sm, ws, in, in_off, in_bias, out, out_off, out_bias, out_len, status, s, cnt, lane);
       else
-        decode_tile_long(sm, ws, in, in_off, in_bias, out, out_off, out_bias, out_len, status, s, cnt, lane);
+        decode_tile_long<kGaps>(sm, ws, in, in_off, in_end, in_bias, out, out_off, out_bias, out_len, status, s,
+                                cnt, lane);
     }
     TL(5 + 5 * (int)tl_j);
     tl_j++;
@@ -1114,10 +1160,10 @@ extern "C" int mhq_diag_timeline(unsigned long long *out, int n) {
 
 hipError_t launch_decode(const DevTables &t, const uint8_t *in, const uint64_t *in_off, uint64_t in_bias,
                          uint64_t n, uint8_t *out, const uint64_t *out_off, uint64_t out_bias,
-                         uint32_t *out_len, uint8_t *status, hipStream_t s) {
+                         uint32_t *out_len, uint8_t *status, hipStream_t s, const uint64_t *in_end) {
   if (n == 0) return hipSuccess;
 #ifdef MHQ_DEC_WG
-  return launch_decode_wg(t, in, in_off, in_bias, n, out, out_off, out_bias, out_len, status, s);
+  if (!in_end) return launch_decode_wg(t, in, in_off, in_bias, n, out, out_off, out_bias, out_len, status, s);
 #endif
   // One workgroup per CU, each a contiguous range of whole wave tiles.  The
   // tile length (<= kTile) is chosen so that every wave gets the same number
@@ -1130,8 +1176,14 @@ hipError_t launch_decode(const DevTables &t, const uint8_t *in, const uint64_t *
   const uint64_t tl = std::max<uint64_t>(1, (n + slots * rounds - 1) / (slots * rounds));
   const uint64_t per_block = (((n + cus - 1) / cus + tl - 1) / tl) * tl;
   const unsigned grid = (unsigned)((n + per_block - 1) / per_block);
-  decode_kernel<<<dim3(grid), dim3(kT), 0, s>>>(in, in_off, in_bias, n, out, out_off, out_bias, out_len, status,
-                                                 t.lut1, t.lut2, t.len, per_block, (uint32_t)tl);
+  if (in_end)
+    decode_kernel<true><<<dim3(grid), dim3(kT), 0, s>>>(in, in_off, in_end, in_bias, n, out, out_off, out_bias,
+                                                        out_len, status, t.lut1, t.lut2, t.len, per_block,
+                                                        (uint32_t)tl);
+  else
+    decode_kernel<false><<<dim3(grid), dim3(kT), 0, s>>>(in, in_off, nullptr, in_bias, n, out, out_off, out_bias,
+                                                         out_len, status, t.lut1, t.lut2, t.len, per_block,
+                                                         (uint32_t)tl);
   return hipGetLastError();
 }
 

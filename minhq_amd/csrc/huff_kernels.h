@@ -35,9 +35,13 @@ hipError_t launch_offsets_sums(const uint32_t *enc_len, uint64_t n, uint64_t *bl
 hipError_t launch_encode(const DevTables &t, const uint8_t *in, const uint64_t *in_off,
                          uint64_t in_bias, uint64_t n, uint8_t *out, const uint64_t *out_off,
                          uint64_t out_bias, hipStream_t s);
+// in_end (optional): literal i is in[in_off[i] - in_bias .. in_end[i] - in_bias),
+// in_end[i] <= in_off[i + 1] when the literals are in order (any order decodes;
+// in-order tiles are the fast ones), in_off[n] >= every in_end.
 hipError_t launch_decode(const DevTables &t, const uint8_t *in, const uint64_t *in_off,
                          uint64_t in_bias, uint64_t n, uint8_t *out, const uint64_t *out_off,
-                         uint64_t out_bias, uint32_t *out_len, uint8_t *status, hipStream_t s);
+                         uint64_t out_bias, uint32_t *out_len, uint8_t *status, hipStream_t s,
+                         const uint64_t *in_end = nullptr);
 // The workgroup-cooperative decode (huff_decode_wg.hip); same contract.
 hipError_t launch_decode_wg(const DevTables &t, const uint8_t *in, const uint64_t *in_off,
                             uint64_t in_bias, uint64_t n, uint8_t *out, const uint64_t *out_off,

@@ -23,38 +23,18 @@ inline unsigned blocks(uint64_t n) { return (unsigned)((n + kT - 1) / kT); }
 
 // Per-string parse state between the read kernels.
 struct ReadScratch {
-  uint64_t *start;  // payload start (byte index into blk)
-  uint64_t *take;   // payload bytes inside the block (the LimitedReader, truncated at limit)
-  uint64_t *declared;
+  uint64_t *start;  // payload start (byte index into blk); start[n] = blk_len (the decode's in_off)
+  uint64_t *hend;   // Huffman payload end: start + take for a Huffman string, start otherwise (in_end)
   uint32_t *cap;    // output capacity: floor(8*take/5) (Huffman) or take (raw)
-  uint32_t *hsz;    // Huffman payload bytes (0 for raw strings)
-  uint8_t *kind;    // 0 raw, 1 Huffman, 2 header error (hc/io.go:74-81 return ("", nil))
+  uint8_t *kind;    // 0 raw, 1 Huffman, 2 header error (hc/io.go:74-81 return ("", nil)); | kDeclared
 };
+constexpr uint8_t kDeclared = 4;  // the declared length is not 0
 
 // Reader.ReadBit + Reader.ReadInt(prefix) at byte pos, bit 7-prefix being the
 // H bit, reading no byte at or past limit (hc/io.go:25-55, 73-81).
-// Each block also writes the (capacity, Huffman size) sums of its kT strings
+// Each block also writes the capacity sums of its strings, per kLenSumBlock,
 // to block_sums: the offsets scan's first pass.
-__device__ __forceinline__ void block_sums2(uint64_t a, uint64_t b, uint64_t *__restrict__ block_sums) {
-  __shared__ uint64_t part[2 * (kT / 64)];
-  const uint32_t lane = threadIdx.x % 64, wave = threadIdx.x / 64;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    a += __shfl_xor(a, d);
-    b += __shfl_xor(b, d);
-  }
-  if (lane == 0) {
-    part[2 * wave] = a;
-    part[2 * wave + 1] = b;
-  }
-  __syncthreads();
-  if (threadIdx.x < 2) {
-    uint64_t v = 0;
-#pragma unroll
-    for (int w = 0; w < kT / 64; w++) v += part[2 * w + threadIdx.x];
-    block_sums[2 * blockIdx.x + threadIdx.x] = v;
-  }
-}
+constexpr int kParsePer = 4;  // strings per parse thread: i = block * kT * kParsePer + k * kT + tid
 
 __global__ __launch_bounds__(kT) void read_parse_kernel(const uint8_t *__restrict__ blk, uint64_t blk_len,
                                                         const uint64_t *__restrict__ pos,
@@ -62,55 +42,87 @@ __global__ __launch_bounds__(kT) void read_parse_kernel(const uint8_t *__restric
                                                         const uint8_t *__restrict__ prefix, uint64_t n,
                                                         ReadScratch sc, uint64_t *__restrict__ next,
                                                         uint64_t *__restrict__ block_sums) {
-  static_assert(kT == kLenSumBlock, "block sums per kLenSumBlock strings");
-  const uint64_t i = (uint64_t)blockIdx.x * kT + threadIdx.x;
-  if (i >= n) {
-    block_sums2(0, 0, block_sums);
-    return;
+  static_assert(kT == kLenSumBlock, "block sums per kLenSumBlock strings: one per k");
+  // Every load of the thread's strings is issued before the first one is
+  // used (the per-string chain pos -> header octet is two dependent loads).
+  const uint64_t i0 = (uint64_t)blockIdx.x * (kT * kParsePer) + threadIdx.x;
+  uint64_t p0[kParsePer], lim[kParsePer];
+  uint32_t pf[kParsePer], b0[kParsePer];
+#pragma unroll
+  for (int k = 0; k < kParsePer; k++) {
+    const uint64_t i = i0 + (uint64_t)k * kT;
+    const uint64_t j = i < n ? i : n - 1;  // (clamped: loads stay inside the arrays)
+    p0[k] = pos[j];
+    lim[k] = min(limit[j], blk_len);  // a limit past the block is the block's end: no byte past blk_len is read
+    pf[k] = prefix[j];
   }
-  // a limit past the block is the block's end: no byte past blk_len is read
-  const uint64_t p0 = pos[i], lim = min(limit[i], blk_len);
-  const uint32_t pf = prefix[i];
-  uint8_t kind = 2;
-  uint64_t start = p0, take = 0, v = 0;
-  if (pf >= 1 && pf <= 7 && p0 < lim) {
-    const uint32_t b0 = blk[p0];
-    const uint32_t h = (b0 >> pf) & 1u;
-    const uint64_t mask = (1ull << pf) - 1u;
-    v = b0 & mask;
-    uint64_t q = p0 + 1;
-    bool ok = true;
-    if (v == mask) {
-      for (uint32_t s = 0; s < 64; s += 7) {
-        if (q >= lim) {  // EOF inside the integer
-          ok = false;
-          break;
+#pragma unroll
+  for (int k = 0; k < kParsePer; k++) b0[k] = p0[k] < lim[k] ? blk[p0[k]] : 0u;
+  uint32_t caps[kParsePer];
+#pragma unroll
+  for (int k = 0; k < kParsePer; k++) {
+    const uint64_t i = i0 + (uint64_t)k * kT;
+    caps[k] = 0;
+    if (i >= n) continue;
+    uint8_t kind = 2;
+    uint64_t start = p0[k], take = 0, v = 0;
+    if (pf[k] >= 1 && pf[k] <= 7 && p0[k] < lim[k]) {
+      const uint32_t h = (b0[k] >> pf[k]) & 1u;
+      const uint64_t mask = (1ull << pf[k]) - 1u;
+      v = b0[k] & mask;
+      uint64_t q = p0[k] + 1;
+      bool ok = true;
+      if (v == mask) {
+        for (uint32_t sh = 0; sh < 64; sh += 7) {
+          if (q >= lim[k]) {  // EOF inside the integer
+            ok = false;
+            break;
+          }
+          const uint64_t b = blk[q++];
+          if (sh == 63 && (b > 1 || (b == 1 && (v >> 63) == 1))) {  // ErrIntegerOverflow (hc/io.go:46)
+            ok = false;
+            break;
+          }
+          v += (b & 0x7f) << sh;
+          if ((b & 0x80) == 0) break;
         }
-        const uint64_t b = blk[q++];
-        if (s == 63 && (b > 1 || (b == 1 && (v >> 63) == 1))) {  // ErrIntegerOverflow (hc/io.go:46)
-          ok = false;
-          break;
-        }
-        v += (b & 0x7f) << s;
-        if ((b & 0x80) == 0) break;
+      }
+      if (ok) {
+        kind = (uint8_t)h;
+        start = q;
+        const uint64_t avail = lim[k] - q;
+        take = v < avail ? v : avail;
       }
     }
-    if (ok) {
-      kind = (uint8_t)h;
-      start = q;
-      const uint64_t avail = lim - q;
-      take = v < avail ? v : avail;
+    sc.start[i] = start;
+    sc.hend[i] = kind == 1 ? start + take : start;
+    if (i == n - 1) sc.start[n] = blk_len;
+    sc.kind[i] = kind | (kind != 2 && v != 0 ? kDeclared : 0);
+    caps[k] = kind == 1 ? (uint32_t)(take * 8 / 5) : (uint32_t)take;
+    sc.cap[i] = caps[k];
+    next[i] = kind == 2 ? p0[k] : start + take;
+  }
+  // (sum of cap, sum of cap) per kLenSumBlock strings: group k of this block
+  __shared__ uint64_t part[kParsePer][kT / 64];
+  const uint32_t lane = threadIdx.x % 64, wave = threadIdx.x / 64;
+#pragma unroll
+  for (int k = 0; k < kParsePer; k++) {
+    uint64_t a = caps[k];
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) a += __shfl_xor(a, d);
+    if (lane == 0) part[k][wave] = a;
+  }
+  __syncthreads();
+  if (threadIdx.x < kParsePer) {
+    const uint64_t g = (uint64_t)blockIdx.x * kParsePer + threadIdx.x;
+    if (g * kT < n) {
+      uint64_t v = 0;
+#pragma unroll
+      for (int w = 0; w < kT / 64; w++) v += part[threadIdx.x][w];
+      block_sums[2 * g] = v;
+      block_sums[2 * g + 1] = v;
     }
   }
-  sc.start[i] = start;
-  sc.take[i] = take;
-  sc.declared[i] = kind == 2 ? 0 : v;
-  sc.kind[i] = kind;
-  const uint32_t cap = kind == 1 ? (uint32_t)(take * 8 / 5) : (uint32_t)take, hsz = kind == 1 ? (uint32_t)take : 0u;
-  sc.cap[i] = cap;
-  sc.hsz[i] = hsz;
-  next[i] = kind == 2 ? p0 : start + take;
-  block_sums2(cap, hsz, block_sums);
 }
 
 // len bytes from src to dst, any alignments, by one thread: the 0-3 bytes up
@@ -153,96 +165,59 @@ __device__ __forceinline__ void copy_bytes(uint8_t *__restrict__ dst, const uint
   }
 }
 
-// Huffman payloads into the packed decode input (hin[hin_off[i]..]), a wave
-// per 64 strings.  Their packed destination is one contiguous range, and in a
-// block of consecutive fields their sources are too (payloads separated by
-// the next field's header octets): when both fit kGatherWin bytes, the wave
-// stages the source span into LDS with aligned 16-B loads, each lane moves
-// its payload inside LDS, and the destination leaves as aligned 16-B stores,
-// so global memory sees whole-wave coalesced accesses instead of 64 lanes'
-// scattered dwords.  Other waves (long, overlapping or out-of-order payloads)
-// copy lane by lane from global memory.
-#ifndef MHQ_GATHER_WIN  // bytes of a wave's source / destination window (LDS: 2 per wave)
-#define MHQ_GATHER_WIN 2048
-#endif
-constexpr uint32_t kGatherWin = MHQ_GATHER_WIN;
-constexpr int kGatherWaves = kT / 64;
-
-__global__ __launch_bounds__(kT) void gather_huff_kernel(const uint8_t *__restrict__ blk, ReadScratch sc, uint64_t n,
-                                                         const uint64_t *__restrict__ hin_off,
-                                                         uint8_t *__restrict__ hin) {
-  __shared__ __attribute__((aligned(16))) uint8_t win[kGatherWaves][2][kGatherWin];
-  const uint32_t lane = threadIdx.x % 64, wave = threadIdx.x / 64;
-  const uint64_t s0 = (uint64_t)blockIdx.x * kT + (uint64_t)wave * 64;
-  if (s0 >= n) return;
-  const uint64_t i = s0 + lane;
-  const bool live = i < n && sc.kind[i] == 1;
-  const uint64_t d = live ? hin_off[i] : 0, len = live ? hin_off[i + 1] - d : 0;  // clamped: 0 past the scratch
-  const uint64_t src = live ? sc.start[i] : 0;
-  // the wave's source span and destination range
-  uint64_t lo = len ? src : ~0ull, hi = len ? src + len : 0;
-#pragma unroll
-  for (int k = 1; k < 64; k <<= 1) {
-    lo = min(lo, (uint64_t)__shfl_xor((unsigned long long)lo, k));
-    hi = max(hi, (uint64_t)__shfl_xor((unsigned long long)hi, k));
-  }
-  if (hi == 0) return;  // nothing to move (uniform)
-  const uint64_t d0 = hin_off[s0], d1 = hin_off[min(s0 + 64, n)];
-  // aligned bases by pointer arithmetic (global, not flat, memory operations)
-  const uint8_t *sb8 = blk + lo - ((uintptr_t)(blk + lo) & 15u);
-  uint8_t *db8 = hin + d0 - ((uintptr_t)(hin + d0) & 15u);
-  const uintptr_t sb = (uintptr_t)sb8, db = (uintptr_t)db8;
-  const uint64_t sspan = (uintptr_t)(blk + hi) - sb, dspan = (uintptr_t)(hin + d1) - db;
-  if (sspan > kGatherWin || dspan > kGatherWin) {
-    if (len) copy_bytes(hin + d, blk + src, len);
-    return;
-  }
-  uint8_t *ws = win[wave][0], *wd = win[wave][1];
-  const uint32_t nck = (uint32_t)((sspan + 15) >> 4);  // aligned chunks holding a byte of the span
-  for (uint32_t c = lane; c < nck; c += 64)
-    *(dev::u32x4 *)(ws + 16u * c) = __builtin_nontemporal_load((const dev::u32x4 *)sb8 + c);
-  dev::wave_sync();
-  if (len) copy_bytes(wd + ((uintptr_t)(hin + d) - db), ws + ((uintptr_t)(blk + src) - sb), len);
-  dev::wave_sync();
-  dev::store_out(db8, wd, (uint32_t)((uintptr_t)(hin + d0) - db), (uint32_t)dspan, (int)lane);
-}
-
 // Raw payloads into the output (after the decode, which zero-fills the
 // regions it stages), then the per-string outcome of hc/io.go:92-96.
-__global__ void read_finish_kernel(const uint8_t *__restrict__ blk, ReadScratch sc, uint64_t n,
-                                   const uint64_t *__restrict__ out_off, const uint64_t *__restrict__ hin_off,
-                                   uint8_t *__restrict__ out, uint32_t *__restrict__ out_len,
-                                   uint8_t *__restrict__ status) {
-  const uint64_t i = (uint64_t)blockIdx.x * kT + threadIdx.x;
-  if (i >= n) return;
-  const uint8_t kind = sc.kind[i];
-  const uint64_t room = out_off[i + 1] - out_off[i];
-  uint8_t st = MHQ_STR_OK;
-  uint32_t len = 0;
-  if (kind == 2) {  // ReadBit / ReadInt failed: ("", nil)
-  } else if (room < sc.cap[i] || hin_off[i + 1] - hin_off[i] < sc.hsz[i]) {
-    // the output region, or the packed Huffman input (overlapping payloads
-    // can total more than the block), was cut short by the buffer's end
-    st = MHQ_STR_NOSPACE;
-  } else if (kind == 1) {
-    len = out_len[i];
-    if (status[i] == MHQ_LIT_INVALID) {
-      st = MHQ_STR_INVALID;  // ("", "invalid Huffman coding")
-      len = 0;
-    } else if (len == 0) {
-      st = MHQ_STR_EOF;  // io.ReadFull into len*8/5+1 >= 1 bytes read nothing: io.EOF
-    }
-  } else {
-    const uint64_t take = sc.take[i];
-    if (take == 0 && sc.declared[i] > 0) {
-      st = MHQ_STR_EOF;  // the block ended before the payload: io.EOF
-    } else {
-      copy_bytes(out + out_off[i], blk + sc.start[i], take);
-      len = (uint32_t)take;
-    }
+__global__ __launch_bounds__(kT) void read_finish_kernel(const uint8_t *__restrict__ blk, ReadScratch sc, uint64_t n,
+                                                         const uint64_t *__restrict__ out_off,
+                                                         const uint64_t *__restrict__ next,
+                                                         uint8_t *__restrict__ out, uint32_t *__restrict__ out_len,
+                                                         uint8_t *__restrict__ status) {
+  // kParsePer strings per thread as in read_parse_kernel, all loads first
+  const uint64_t i0 = (uint64_t)blockIdx.x * (kT * kParsePer) + threadIdx.x;
+  uint8_t kd[kParsePer], ds[kParsePer];
+  uint64_t o0[kParsePer], o1[kParsePer];
+  uint32_t cap[kParsePer], dl[kParsePer];
+#pragma unroll
+  for (int k = 0; k < kParsePer; k++) {
+    const uint64_t i = i0 + (uint64_t)k * kT;
+    const uint64_t j = i < n ? i : n - 1;
+    kd[k] = sc.kind[j];
+    o0[k] = out_off[j];
+    o1[k] = out_off[j + 1];
+    cap[k] = sc.cap[j];
+    dl[k] = out_len[j];
+    ds[k] = status[j];
   }
-  out_len[i] = len;
-  status[i] = st;
+#pragma unroll
+  for (int k = 0; k < kParsePer; k++) {
+    const uint64_t i = i0 + (uint64_t)k * kT;
+    if (i >= n) continue;
+    const uint8_t kind = kd[k] & 3u;
+    uint8_t st = MHQ_STR_OK;
+    uint32_t len = 0;
+    if (kind == 2) {                   // ReadBit / ReadInt failed: ("", nil)
+    } else if (o1[k] - o0[k] < cap[k]) {  // the output region was cut short by the buffer's end
+      st = MHQ_STR_NOSPACE;
+    } else if (kind == 1) {
+      len = dl[k];
+      if (ds[k] == MHQ_LIT_INVALID) {
+        st = MHQ_STR_INVALID;  // ("", "invalid Huffman coding")
+        len = 0;
+      } else if (len == 0) {
+        st = MHQ_STR_EOF;  // io.ReadFull into len*8/5+1 >= 1 bytes read nothing: io.EOF
+      }
+    } else {
+      const uint64_t start = sc.start[i], take = next[i] - start;  // next = start + take (kind 0)
+      if (take == 0 && (kd[k] & kDeclared)) {
+        st = MHQ_STR_EOF;  // the block ended before the payload: io.EOF
+      } else {
+        copy_bytes(out + o0[k], blk + start, take);
+        len = (uint32_t)take;
+      }
+    }
+    out_len[i] = len;
+    status[i] = st;
+  }
 }
 
 // ---- write side ----------------------------------------------------------
@@ -512,7 +487,7 @@ namespace {
 
 // read_strings' scratch, 16-B aligned pieces of one allocation.
 struct ReadLayout {
-  size_t start, take, declared, cap, hsz, kind, hin_off, sums, hin, total;
+  size_t start, hend, cap, kind, sums, total;
   ReadLayout(uint64_t n, uint64_t blk_len) {
     size_t o = 0;
     auto take_ = [&](size_t bytes) {
@@ -520,15 +495,11 @@ struct ReadLayout {
       o += (bytes + 15) & ~(size_t)15;
       return at;
     };
-    start = take_(8 * n);
-    take = take_(8 * n);
-    declared = take_(8 * n);
+    start = take_(8 * (n + 1));
+    hend = take_(8 * n);
     cap = take_(4 * n);
-    hsz = take_(4 * n);
     kind = take_(n);
-    hin_off = take_(8 * (n + 1));
     sums = take_(offsets_sums_scratch_bytes(n));
-    hin = take_(blk_len + 16);
     total = o;
   }
 };
@@ -537,8 +508,9 @@ struct ReadLayout {
 
 size_t read_strings_scratch_bytes(uint64_t n, uint64_t blk_len) { return ReadLayout(n, blk_len).total; }
 
-// parse (+ block sums) -> one scan of (capacity, Huffman size) into out_off / hin_off, each
-// clamped to its buffer -> gather of the Huffman payloads -> decode -> finish.
+// parse (+ block sums) -> one scan of the capacities into out_off, clamped to
+// the output -> decode of the Huffman payloads where they lie in the block
+// (launch_decode with in_end) -> finish.
 hipError_t launch_read_strings(const DevTables &t, const uint8_t *blk, uint64_t blk_len, const uint64_t *pos,
                                const uint64_t *limit, const uint8_t *prefix, uint64_t n, uint8_t *out,
                                uint64_t out_cap, uint64_t *out_off, uint32_t *out_len, uint8_t *status,
@@ -550,25 +522,21 @@ hipError_t launch_read_strings(const DevTables &t, const uint8_t *blk, uint64_t 
   uint8_t *base = (uint8_t *)scratch;
   hipError_t e = hipSuccess;
   if (!base && (e = hipMallocAsync((void **)&base, L.total, s)) != hipSuccess) return e;
-  ReadScratch sc{(uint64_t *)(base + L.start), (uint64_t *)(base + L.take), (uint64_t *)(base + L.declared),
-                 (uint32_t *)(base + L.cap), (uint32_t *)(base + L.hsz), base + L.kind};
-  uint64_t *hin_off = (uint64_t *)(base + L.hin_off);
-  uint8_t *hin = base + L.hin;
+  ReadScratch sc{(uint64_t *)(base + L.start), (uint64_t *)(base + L.hend), (uint32_t *)(base + L.cap),
+                 base + L.kind};
 #define TRY(x)                   \
   do {                           \
     e = (x);                     \
     if (e != hipSuccess) goto done; \
   } while (0)
-  read_parse_kernel<<<blocks(n), kT, 0, s>>>(blk, blk_len, pos, limit, prefix, n, sc, next,
+  read_parse_kernel<<<(unsigned)((n + kT * kParsePer - 1) / (kT * kParsePer)), kT, 0, s>>>(blk, blk_len, pos, limit, prefix, n, sc, next,
                                              (uint64_t *)(base + L.sums));
   TRY(hipGetLastError());
-  // output regions: capacities back to back; the packed Huffman input
-  TRY(launch_offsets_pair_sums(sc.cap, sc.hsz, n, (uint64_t *)(base + L.sums), out_cap, blk_len, out_off, hin_off,
+  // output regions: capacities back to back
+  TRY(launch_offsets_pair_sums(sc.cap, sc.cap, n, (uint64_t *)(base + L.sums), out_cap, out_cap, out_off, nullptr,
                                s));
-  gather_huff_kernel<<<blocks(n), kT, 0, s>>>(blk, sc, n, hin_off, hin);
-  TRY(hipGetLastError());
-  TRY(launch_decode(t, hin, hin_off, 0, n, out, out_off, 0, out_len, status, s));
-  read_finish_kernel<<<blocks(n), kT, 0, s>>>(blk, sc, n, out_off, hin_off, out, out_len, status);
+  TRY(launch_decode(t, blk, sc.start, 0, n, out, out_off, 0, out_len, status, s, sc.hend));
+  read_finish_kernel<<<(unsigned)((n + kT * kParsePer - 1) / (kT * kParsePer)), kT, 0, s>>>(blk, sc, n, out_off, next, out, out_len, status);
   TRY(hipGetLastError());
 done:
   if (!scratch) {
