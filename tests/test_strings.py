@@ -163,3 +163,64 @@ def test_read_overlapping_payloads(codec, oracle_mod):
     NOSPACE = 3
     assert all((v, int(s)) == (ref, OK) or int(s) == NOSPACE for v, s in zip(vals, st))
     assert int(st[0]) == OK and vals[0] == ref
+
+
+@pytest.mark.parametrize("order", ["in_order", "shuffled", "runs"])
+def test_read_gaps_and_order(codec, oracle_mod, order):
+    """The decode reads the Huffman payloads where they lie in the block
+    (str_frame.hip, launch_decode with in_end): fields separated by other
+    octets (gaps), read in block order (tiles staged), in a random order
+    (every tile streams), or in shuffled runs of 300 (both kinds of tile).
+    Each string against the oracle's ReadString from its position."""
+    rng = random.Random({"in_order": 31, "shuffled": 32, "runs": 33}[order])
+    strs = _random_strings(rng, 20000)
+    blk, pos, prefixes = bytearray(), [], []
+    for s in strs:
+        blk += bytes(rng.randrange(256) for _ in range(rng.choice([0, 0, 1, 3, 9])))  # a gap
+        p = rng.choice([7, 5, 3])
+        pos.append(len(blk))
+        prefixes.append(p)
+        blk += oracle_mod.write_string(s, prefix=p, choice=rng.choice([1, 1, 1, 2, 0]),
+                                       lead=rng.randrange(1 << (7 - p)) if p < 7 else 0, lead_bits=7 - p)
+    blk = bytes(blk)
+    idx = list(range(len(strs)))
+    if order == "shuffled":
+        rng.shuffle(idx)
+    elif order == "runs":
+        runs = [idx[k:k + 300] for k in range(0, len(idx), 300)]
+        rng.shuffle(runs)
+        idx = [i for r in runs for i in r]
+    P = [pos[i] for i in idx]
+    F = [prefixes[i] for i in idx]
+    vals, st, nxt = codec.read_strings(blk, P, F)
+    for k, i in enumerate(idx):
+        ref, rc, used = oracle_mod.read_string(blk[pos[i]:], prefix=prefixes[i], skip_bits=7 - prefixes[i])
+        assert (vals[k], int(st[k])) == (ref, _oracle_status(rc)), (order, k, i)
+        assert int(nxt[k]) == pos[i] + used
+
+
+def test_read_gaps_full_tiles(codec, oracle_mod):
+    """Full-size decode tiles over a block with gaps (in order: staged with the
+    ends kept apart from the next starts); a sample of strings and every
+    status/next against the oracle."""
+    import numpy as np
+
+    rng = random.Random(34)
+    alpha = b"abcdefghijklmnopqrstuvwxyz0123456789-_./:;=, "
+    n = 1 << 18
+    blk, pos = bytearray(), []
+    pieces = [oracle_mod.write_string(bytes(rng.choice(alpha) for _ in range(rng.randint(1, 40))), prefix=7,
+                                      choice=1) for _ in range(4096)]
+    for k in range(n):
+        if rng.random() < 0.3:
+            blk += b"\x82\x90"[: rng.randint(1, 2)]  # other instructions' octets between the fields
+        pos.append(len(blk))
+        blk += pieces[rng.randrange(len(pieces))] if rng.random() < 0.97 else bytes([0x03]) + b"raw"
+    blk = bytes(blk)
+    vals, st, nxt = codec.read_strings(blk, pos, [7] * n)
+    sample = sorted(rng.sample(range(n), 20000))
+    for i in sample:
+        ref, rc, used = oracle_mod.read_string(blk[pos[i]:pos[i] + 200], prefix=7)
+        assert (vals[i], int(st[i])) == (ref, _oracle_status(rc)), i
+        assert int(nxt[i]) == pos[i] + used
+    assert (np.asarray(st) == OK).all()
