@@ -233,7 +233,7 @@ def main():
         assert int(s["st"].sum().item()) == 0
         assert torch.equal(s["len"].long(), off[1:] - off[:-1])
     alg = {"decode": enc_bytes + b.nbytes + 16 * (n + 1) + 5 * n,
-           "encode": b.nbytes + enc_bytes + 16 * (n + 1),
+           "encode": b.nbytes + enc_bytes + 16 * (n + 1) + 4 * n,  # + 4n (enc_len)
            "encode_len": b.nbytes + 8 * (n + 1) + 4 * n, "offsets": 4 * n + 16 * (n + 1),
            "layout": b.nbytes + 8 * (n + 1) + 8 * n + 16 * (n + 1)}[args.kernel]
     print(json.dumps({"kernel": args.kernel, "config": b.name, "n": n, "plain": b.nbytes, "enc": enc_bytes,
