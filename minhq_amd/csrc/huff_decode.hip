@@ -53,6 +53,9 @@
 #ifndef MHQ_DEC_XROUNDS  // tile rounds beyond the fewest that hold the batch (smaller tiles, more of them)
 #define MHQ_DEC_XROUNDS 0
 #endif
+#ifndef MHQ_DEC_PRIO  // wave priority during a tile's staging, flush and sort (0: none)
+#define MHQ_DEC_PRIO 3
+#endif
 #ifndef MHQ_DEC_WOUT  // a wave's output slice (bytes, multiple of 16)
 #define MHQ_DEC_WOUT 6448
 #endif
@@ -595,6 +598,9 @@ __device__ __forceinline__ void decode_piece(const Smem &sm, WaveSmem &ws, uint3
   B.load(ws, hasB ? ws.order[2u * kWave - 1u - lane] : 0u);
   const uint32_t ostartA = A.optr, ostartB = B.optr;
   TL(tls);
+#if MHQ_DEC_PRIO
+  __builtin_amdgcn_s_setprio(0);  // the probe loop at normal priority
+#endif
   // Every literal whose region cannot truncate runs the masked loop to its
   // end (ones past the end: no end test, no separate tail loop); the lane
   // moves from A to B in place.  A literal with a code across its end (not
@@ -1071,6 +1077,9 @@ __global__ __launch_bounds__(kT) void decode_kernel(const uint8_t *__restrict__ 
       const bool ok1 = j0 + 1u >= cnt || (c <= re1 && re1 <= (j0 + 2u < cnt ? nx : rie));
       fits = fits && __ballot(!(ok0 && ok1)) == 0;
     }
+#if MHQ_DEC_PRIO
+    __builtin_amdgcn_s_setprio(MHQ_DEC_PRIO);  // staging, flush and sort (serial phases) ahead of other waves' loops
+#endif
     // claim the tile three ahead (used when this one is done)
     uint32_t tile4 = 0;
     if (lane == 0) tile4 = atomicAdd(&sm.next_tile, 1u);
