@@ -56,6 +56,12 @@
 #ifndef MHQ_DEC_PRIO  // wave priority during a tile's staging, flush and sort (0: none)
 #define MHQ_DEC_PRIO 3
 #endif
+#ifndef MHQ_DEC_P3  // a third LUT1 probe per step of the masked loop
+#define MHQ_DEC_P3 0
+#endif
+#ifndef MHQ_DEC_STEPS  // masked steps per end test of the probe loop
+#define MHQ_DEC_STEPS 2
+#endif
 #ifndef MHQ_DEC_WOUT  // a wave's output slice (bytes, multiple of 16)
 #define MHQ_DEC_WOUT 6448
 #endif
@@ -296,6 +302,19 @@ __device__ __forceinline__ bool masked_step(const Smem &sm, uint32_t *otgt, BitB
   e2 = lng ? 0u : e2;
   out.put(e2 >> 16, (e2 >> 8) & 0xffu);
   in.consume(e2);
+#if MHQ_DEC_P3
+  {
+    // a third probe when its codes lie in the buffer's valid bits with two to
+    // spare (the refill then tops up to >= 34) and its bytes fit the 64-bit
+    // accumulator (one word leaves per step)
+    uint32_t e3 = sm.lut1[in.top32() >> (32 - kLut1Bits)];
+    const int32_t nb = in.left - in.rem;
+    const bool take = (int32_t)(e3 & 0xffu) + 2 <= nb && out.ab + ((e3 >> 8) & 0xffu) <= 63u;
+    e3 = take ? e3 : 0u;
+    out.put(e3 >> 16, (e3 >> 8) & 0xffu);
+    in.consume(e3);
+  }
+#endif
   in.refill(w);
   const bool ok = in.left >= 0;
   pend.ow = out.ow;
@@ -554,6 +573,11 @@ template <bool kGaps>
 __device__ __forceinline__ void decode_piece(const Smem &sm, WaveSmem &ws, uint32_t m, uint32_t out_bytes,
                                              uint32_t lane, [[maybe_unused]] int tls = -1) {
   for (uint32_t c = lane; c < (out_bytes + 15u) >> 4; c += kWave) *(u32x4 *)(ws.out_w + 4u * c) = u32x4{0u, 0u, 0u, 0u};
+#ifdef MHQ_X_NOSORT  // timing experiment only: literals in tile order, lane t on t and 127 - t
+  if (lane < m) ws.order[lane] = (uint8_t)lane;
+  if (lane + kWave < m) ws.order[lane + kWave] = (uint8_t)(lane + kWave);
+  wave_sync();
+#else
   // counting sort by encoded length, longest first
   ws.hist[lane] = 0;
   wave_sync();
@@ -582,6 +606,7 @@ __device__ __forceinline__ void decode_piece(const Smem &sm, WaveSmem &ws, uint3
     if (j < m) ws.order[ws.hist[key[h]] + rk[h]] = (uint8_t)j;
   }
   wave_sync();
+#endif
   // Lane t decodes rank t, then rank 127 - t if there is one: the 64 longest
   // literals one per lane, the rest on the lanes with the shortest of those
   // (LPT).  The lane's two fast loops run back to back in one loop (it moves
@@ -628,6 +653,12 @@ __device__ __forceinline__ void decode_piece(const Smem &sm, WaveSmem &ws, uint3
       }
 #endif
       bool stop;
+      // MHQ_DEC_STEPS steps per end test: a finished literal (EOS prefix, or
+      // a code across its end) stays finished through further steps (no bits
+      // consumed at the EOS prefix; `left` stays negative, the word held
+      // back), so the last step's result covers them all
+#pragma unroll
+      for (int k = 1; k < MHQ_DEC_STEPS; k++) masked_step(sm, ws.out_w, in, out, pend, stop);
       if (masked_step(sm, ws.out_w, in, out, pend, stop)) {
         // stop: the EOS prefix at p (INVALID when a 31st bit of the literal follows)
         const uint32_t r = in.left < 0 ? kRedo : (out.optr() - ost) | ((uint32_t)(in.left > kEosOnes) << 31);
