@@ -5,7 +5,8 @@ set -o pipefail
 export TMPDIR=/tmp
 mkdir -p gpurun_out
 for name in ${PARITY_VARIANTS-"$@"}; do
-  MHQ_LIB_PATH=build/var/lib_$name.so timeout -k 10 400 python -u -m pytest ${TESTS:-tests/test_gpu_parity.py tests/test_gpu_stream_path.py tests/test_strings.py} -x -q --timeout 120 --timeout-method thread > gpurun_out/pytest_$name.log 2>&1
+  lib=build/var/lib_$name.so; [ "$name" = default ] && lib=minhq_amd/libmhq_huff.so
+  MHQ_LIB_PATH=$lib timeout -k 10 400 python -u -m pytest ${TESTS:-tests/test_gpu_parity.py tests/test_gpu_stream_path.py tests/test_strings.py} -x -q --timeout 120 --timeout-method thread > gpurun_out/pytest_$name.log 2>&1
   rc=$?; echo "parity $name: $(tail -1 gpurun_out/pytest_$name.log)"; [ $rc -eq 0 ] || exit $rc
 done
 for cfg in ${CONFIGS:-northstar config2}; do
