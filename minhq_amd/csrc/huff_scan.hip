@@ -220,15 +220,28 @@ __global__ __launch_bounds__(kScanBlock) void scan_apply_kernel(F f, uint64_t n,
   uint64_t a[kItems], b[kItems];
   f.load(i0, a, b);
   const uint64_t first = (uint64_t)blockIdx.x * g;  // this chunk's first pair
-  const uint64_t sb = first / kSup;
   uint64_t pa = 0, pb = 0;
-  for (uint64_t j = tid; j < sb; j += kScanBlock) {
-    pa += sup[2 * j];
-    pb += sup[2 * j + 1];
+  if (!sup) {
+    // direct form (few sums, see direct_sums): the raw pairs before this
+    // chunk's first, added up here; no second pass
+    typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+#pragma unroll 4
+    for (uint64_t j = tid; j < first; j += kScanBlock) {
+      const u64x2 v = ((const u64x2 *)sums)[j];
+      pa += v.x;
+      pb += v.y;
+    }
+    block_sum2(pa, pb, sh);
+  } else {
+    const uint64_t sb = first / kSup;
+    for (uint64_t j = tid; j < sb; j += kScanBlock) {
+      pa += sup[2 * j];
+      pb += sup[2 * j + 1];
+    }
+    block_sum2(pa, pb, sh);
+    pa += sums[2 * first];
+    pb += sums[2 * first + 1];
   }
-  block_sum2(pa, pb, sh);
-  pa += sums[2 * first];
-  pb += sums[2 * first + 1];
   uint64_t ta = 0, tb = 0;
 #pragma unroll
   for (int k = 0; k < kItems; k++) {
@@ -291,6 +304,17 @@ __global__ __launch_bounds__(kScanBlock) void scan_apply_kernel(F f, uint64_t n,
 // Superblocks over ns pairs (pair ns included).
 inline uint64_t sup_count(uint64_t ns) { return (ns + 1 + kSup - 1) / kSup; }
 
+// The apply pass adds up the raw sums before its chunk itself (no second
+// pass, one launch fewer) while that reads at most ~32 MB of L2 in all:
+// nb blocks x ns pairs x 16 B / 2 (at 2^20 literals: the layout call's 513
+// chunks over 4,096 encode_len sums; a scan's own 513 reduce sums).
+inline bool direct_sums(uint64_t nb, uint64_t ns) {
+#ifdef MHQ_SCAN_NODIRECT  // timing builds: always the three passes
+  return false;
+#endif
+  return nb * ns <= (1ull << 22);
+}
+
 inline size_t run_scan_bytes(uint64_t n) {
   const uint64_t nb = (n + 1 + kChunk - 1) / kChunk;
   return (size_t)(nb + 1 + sup_count(nb)) * 2 * sizeof(uint64_t);
@@ -308,9 +332,10 @@ hipError_t run_scan(F f, uint64_t n, uint64_t base, uint64_t *oa, uint64_t *ob, 
   if (!sums && (e = hipMallocAsync((void **)&sums, run_scan_bytes(n), s)) != hipSuccess) return e;
   uint64_t *sup = sums + 2 * (nb + 1);
   scan_reduce_kernel<F><<<dim3((unsigned)nb), dim3(kScanBlock), 0, s>>>(f, n, sums);
-  scan_sums_kernel<<<dim3((unsigned)nsup), dim3(kScanBlock), 0, s>>>(sums, nb, sup);
-  scan_apply_kernel<F><<<dim3((unsigned)nb), dim3(kScanBlock), 0, s>>>(f, n, sums, sup, 1u, base, oa, ob, lim_a,
-                                                                        lim_b);
+  const bool direct = direct_sums(nb, nb);
+  if (!direct) scan_sums_kernel<<<dim3((unsigned)nsup), dim3(kScanBlock), 0, s>>>(sums, nb, sup);
+  scan_apply_kernel<F><<<dim3((unsigned)nb), dim3(kScanBlock), 0, s>>>(f, n, sums, direct ? nullptr : sup, 1u, base,
+                                                                        oa, ob, lim_a, lim_b);
   e = hipGetLastError();
   if (scratch) return e;
   hipError_t e2 = hipFreeAsync(sums, s);
@@ -339,9 +364,11 @@ hipError_t launch_offsets_sums(const uint32_t *enc_len, uint64_t n, uint64_t *bl
   const uint64_t ns = (n + kLenSumBlock - 1) / kLenSumBlock;
   const uint64_t nsup = sup_count(ns);
   uint64_t *sup = block_sums + 2 * (ns + 1);
-  scan_sums_kernel<<<dim3((unsigned)nsup), dim3(kScanBlock), 0, s>>>(block_sums, ns, sup);
+  const bool direct = direct_sums(nb, ns);
+  if (!direct) scan_sums_kernel<<<dim3((unsigned)nsup), dim3(kScanBlock), 0, s>>>(block_sums, ns, sup);
   scan_apply_kernel<LenVal><<<dim3((unsigned)nb), dim3(kScanBlock), 0, s>>>(
-      LenVal{enc_len, n}, n, block_sums, sup, (uint32_t)(kChunk / kLenSumBlock), base, out_off, cap_off);
+      LenVal{enc_len, n}, n, block_sums, direct ? nullptr : sup, (uint32_t)(kChunk / kLenSumBlock), base, out_off,
+      cap_off);
   return hipGetLastError();
 }
 
@@ -353,9 +380,11 @@ hipError_t launch_offsets_pair_sums(const uint32_t *a, const uint32_t *b, uint64
   const uint64_t ns = (n + kLenSumBlock - 1) / kLenSumBlock;
   const uint64_t nsup = sup_count(ns);
   uint64_t *sup = block_sums + 2 * (ns + 1);
-  scan_sums_kernel<<<dim3((unsigned)nsup), dim3(kScanBlock), 0, s>>>(block_sums, ns, sup);
+  const bool direct = direct_sums(nb, ns);
+  if (!direct) scan_sums_kernel<<<dim3((unsigned)nsup), dim3(kScanBlock), 0, s>>>(block_sums, ns, sup);
   scan_apply_kernel<PairVal><<<dim3((unsigned)nb), dim3(kScanBlock), 0, s>>>(
-      PairVal{a, b, n}, n, block_sums, sup, (uint32_t)(kChunk / kLenSumBlock), 0, oa, ob, lim_a, lim_b);
+      PairVal{a, b, n}, n, block_sums, direct ? nullptr : sup, (uint32_t)(kChunk / kLenSumBlock), 0, oa, ob, lim_a,
+      lim_b);
   return hipGetLastError();
 }
 

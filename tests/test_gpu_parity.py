@@ -304,12 +304,15 @@ def test_device_resident_round_trip_full_size(codec):
 
 
 @pytest.mark.parametrize("n", [0, 1, 255, 256, 257, 2047, 2048, 2049, 8 * 2048 + 77, 65535, 65536, 65537,
-                               300000, 524287, 524288, 1_100_000])
+                               300000, 524287, 524288, 1_100_000, 2_000_000, 4_500_000])
 def test_encode_layout_matches_two_pass(codec, n):
     """mhq_huff_encode_layout_dev against encode_len_dev + offsets_dev at the
     block-sum edges (256-literal blocks, 2048-item scan chunks, superblocks
     of 256 sums: 65536 literals for the layout call, 2^19 items for the
-    reduce pass), with a base and without cap_off; both against a host scan."""
+    reduce pass), with a base and without cap_off; both against a host scan.
+    Up to ~1.45M literals the layout call's apply pass adds up the sums before
+    its chunk itself, past that the sums pass runs (offsets_dev: past ~4.2M);
+    2M and 4.5M take the three-pass forms."""
     import torch
 
     from minhq_amd import workloads
