@@ -76,6 +76,19 @@ def timeline_report(fn):
         f"{x}:{be[bx == x].mean():.1f}/{be[bx == x].max():.1f}" for x in range(8)) +
         f"  | workgroup end p10 {np.percentile(be, 10):.1f} p50 {np.percentile(be, 50):.1f} max {be.max():.1f}",
         file=sys.stderr)
+    wix = wave_id % 16
+    print("  wave end by wave index (mean): " + " ".join(
+        f"{w}:{end[wix == w].mean():.1f}" for w in range(16) if (wix == w).any()), file=sys.stderr)
+    for j in range(3):
+        b = 1 + 5 * j
+        cols = []
+        for g in range(4):
+            sel = (wix // 4 == g) & (a[:, b + 4] > 0)
+            if sel.any():
+                x = a[sel]
+                cols.append(f"g{g}: issued@{us(x[:, b]).mean():.1f} sorted@{us(x[:, b + 2]).mean():.1f} "
+                            f"loop {(x[:, b + 3] - x[:, b + 2]).mean() / 100:.2f} done@{us(x[:, b + 4]).mean():.1f}")
+        print(f"  tile {j} by age group: " + " | ".join(cols), file=sys.stderr)
     print(f"timeline: {a.shape[0]} waves, start spread {us(a[:, 0]).max():.2f} us, end max {end.max():.2f} "
           f"p50 {np.percentile(end, 50):.2f} p10 {np.percentile(end, 10):.2f} us", file=sys.stderr)
     prev = a[:, 0]
