@@ -165,15 +165,21 @@ __device__ __forceinline__ void copy_bytes(uint8_t *__restrict__ dst, const uint
   }
 }
 
-// Raw payloads into the output (after the decode, which zero-fills the
-// regions it stages), then the per-string outcome of hc/io.go:92-96.
+// Raw payloads into the output (after the decode), then the per-string
+// outcome of hc/io.go:92-96.  The decode has written out_len / status for
+// every string (0 / OK for the raw and unreadable ones, which it sees as
+// empty literals), so only the strings whose outcome differs are written:
+// INVALID (length 0), EOF, raw payloads and cut regions.  Regions are cut
+// short only at the output's end (the scan clamps the offsets to out_cap), so
+// with out_off[n] < out_cap no region is and the capacity test reads nothing.
 __global__ __launch_bounds__(kT) void read_finish_kernel(const uint8_t *__restrict__ blk, ReadScratch sc, uint64_t n,
                                                          const uint64_t *__restrict__ out_off,
                                                          const uint64_t *__restrict__ next,
                                                          uint8_t *__restrict__ out, uint32_t *__restrict__ out_len,
-                                                         uint8_t *__restrict__ status) {
+                                                         uint8_t *__restrict__ status, uint64_t out_cap) {
   // kParsePer strings per thread as in read_parse_kernel, all loads first
   const uint64_t i0 = (uint64_t)blockIdx.x * (kT * kParsePer) + threadIdx.x;
+  const bool clamped = out_off[n] >= out_cap;  // (uniform)
   uint8_t kd[kParsePer], ds[kParsePer];
   uint64_t o0[kParsePer], o1[kParsePer];
   uint32_t cap[kParsePer], dl[kParsePer];
@@ -182,41 +188,41 @@ __global__ __launch_bounds__(kT) void read_finish_kernel(const uint8_t *__restri
     const uint64_t i = i0 + (uint64_t)k * kT;
     const uint64_t j = i < n ? i : n - 1;
     kd[k] = sc.kind[j];
-    o0[k] = out_off[j];
-    o1[k] = out_off[j + 1];
-    cap[k] = sc.cap[j];
     dl[k] = out_len[j];
     ds[k] = status[j];
+    o0[k] = o1[k] = 0;
+    cap[k] = 0;
+    if (clamped) {
+      o0[k] = out_off[j];
+      o1[k] = out_off[j + 1];
+      cap[k] = sc.cap[j];
+    }
   }
 #pragma unroll
   for (int k = 0; k < kParsePer; k++) {
     const uint64_t i = i0 + (uint64_t)k * kT;
     if (i >= n) continue;
     const uint8_t kind = kd[k] & 3u;
-    uint8_t st = MHQ_STR_OK;
-    uint32_t len = 0;
-    if (kind == 2) {                   // ReadBit / ReadInt failed: ("", nil)
-    } else if (o1[k] - o0[k] < cap[k]) {  // the output region was cut short by the buffer's end
-      st = MHQ_STR_NOSPACE;
+    if (kind == 2) continue;  // ReadBit / ReadInt failed: ("", nil), as the decode left it
+    if (o1[k] - o0[k] < cap[k]) {  // the output region was cut short by the buffer's end
+      out_len[i] = 0;
+      status[i] = MHQ_STR_NOSPACE;
     } else if (kind == 1) {
-      len = dl[k];
-      if (ds[k] == MHQ_LIT_INVALID) {
-        st = MHQ_STR_INVALID;  // ("", "invalid Huffman coding")
-        len = 0;
-      } else if (len == 0) {
-        st = MHQ_STR_EOF;  // io.ReadFull into len*8/5+1 >= 1 bytes read nothing: io.EOF
+      if (ds[k] == MHQ_LIT_INVALID) {  // ("", "invalid Huffman coding"): MHQ_STR_INVALID, length 0
+        if (dl[k] != 0) out_len[i] = 0;
+      } else if (dl[k] == 0) {
+        status[i] = MHQ_STR_EOF;  // io.ReadFull into len*8/5+1 >= 1 bytes read nothing: io.EOF
       }
     } else {
       const uint64_t start = sc.start[i], take = next[i] - start;  // next = start + take (kind 0)
       if (take == 0 && (kd[k] & kDeclared)) {
-        st = MHQ_STR_EOF;  // the block ended before the payload: io.EOF
-      } else {
-        copy_bytes(out + o0[k], blk + start, take);
-        len = (uint32_t)take;
+        status[i] = MHQ_STR_EOF;  // the block ended before the payload: io.EOF
+      } else if (take) {
+        const uint64_t ob = clamped ? o0[k] : out_off[i];
+        copy_bytes(out + ob, blk + start, take);
+        out_len[i] = (uint32_t)take;
       }
     }
-    out_len[i] = len;
-    status[i] = st;
   }
 }
 
@@ -536,7 +542,7 @@ hipError_t launch_read_strings(const DevTables &t, const uint8_t *blk, uint64_t 
   TRY(launch_offsets_pair_sums(sc.cap, sc.cap, n, (uint64_t *)(base + L.sums), out_cap, out_cap, out_off, nullptr,
                                s));
   TRY(launch_decode(t, blk, sc.start, 0, n, out, out_off, 0, out_len, status, s, sc.hend));
-  read_finish_kernel<<<(unsigned)((n + kT * kParsePer - 1) / (kT * kParsePer)), kT, 0, s>>>(blk, sc, n, out_off, next, out, out_len, status);
+  read_finish_kernel<<<(unsigned)((n + kT * kParsePer - 1) / (kT * kParsePer)), kT, 0, s>>>(blk, sc, n, out_off, next, out, out_len, status, out_cap);
   TRY(hipGetLastError());
 done:
   if (!scratch) {
