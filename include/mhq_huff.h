@@ -153,8 +153,9 @@ int mhq_read_strings_dev(mhq_ctx *ctx, int dev, const uint8_t *blk, uint64_t blk
  * 7-prefix[i] bits above the H bit).  Writes out_off[0..n] (frame i is
  * out[out_off[i]..out_off[i+1])) and, when out is not NULL, the frames and
  * status[i] (MHQ_STR_OK, or MHQ_STR_NOSPACE past out_cap).  With out NULL only
- * out_off is computed (size query).  Synchronises `stream` once (to size the
- * Huffman scratch).  Device pointers. */
+ * out_off is computed (size query).  Device pointers; asynchronous on `stream`
+ * (no synchronisation inside: only payloads whose frames fit out_cap are
+ * encoded, into scratch sized from out_cap). */
 int mhq_write_strings_dev(mhq_ctx *ctx, int dev, const uint8_t *in, const uint64_t *in_off, uint64_t n,
                           const uint8_t *prefix, const uint8_t *lead, int choice, uint8_t *out, uint64_t out_cap,
                           uint64_t *out_off, uint8_t *status, void *stream);
