@@ -45,6 +45,9 @@
 #ifndef MHQ_ENC_BLOCKS  // resident workgroups per CU
 #define MHQ_ENC_BLOCKS 3
 #endif
+#ifndef MHQ_ENC_SHORT_MEAN  // mean plaintext bytes up to which a workgroup takes one range of kT literals
+#define MHQ_ENC_SHORT_MEAN 40
+#endif
 
 namespace mhq {
 namespace {
@@ -56,6 +59,7 @@ constexpr int kInCap = MHQ_ENC_INCAP;
 constexpr int kOutCap = MHQ_ENC_OUTCAP;
 constexpr int kPF = (kInCap / 16 + kT - 1) / kT;  // prefetched input chunks per thread
 constexpr int kBuckets = 64;
+constexpr uint32_t kShortMean = MHQ_ENC_SHORT_MEAN;
 
 template <bool kEmit>
 struct Smem {
@@ -230,19 +234,39 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu((kT / 64 * M
     const uint8_t *__restrict__ in, const uint64_t *__restrict__ in_off, uint64_t in_bias, uint64_t n,
     uint8_t *__restrict__ out, const uint64_t *__restrict__ out_off, uint64_t out_bias,
     uint32_t *__restrict__ enc_len, const uint32_t *__restrict__ g_code, const uint8_t *__restrict__ g_len,
-    uint64_t per_block) {
+    uint64_t per_block, uint32_t n_persist) {
   __shared__ Smem<kEmit> sm;
   const uint32_t tid = threadIdx.x;
   const uint32_t lane = tid % kWave;
   const uint32_t wave = tid / kWave;
-  const uint64_t L0 = (uint64_t)blockIdx.x * per_block;
-  if (L0 >= n) return;
-  const uint64_t L1 = min(L0 + per_block, n);
-  uint64_t cur = L0;
-  uint64_t i_cur = uniform64(vload(in_off, L0)), o_cur = kEmit ? uniform64(vload(out_off, L0)) : 0u;
-  const uint64_t i_end = uniform64(vload(in_off, L1));
+  // Two grids in one launch (the grid holds max(ceil(n / kT), n_persist)
+  // workgroups): short literals (a mean under kShortMean bytes, so kT of them
+  // fill about one staging slice) take one range of kT literals per
+  // workgroup, and the dispatcher refills a CU as its workgroups end; longer
+  // ones take n_persist persistent ranges of per_block literals (greedy
+  // sub-tiles stay full) in the first workgroups, the others ending at once.
+  // The short form's offsets are loaded beside the batch's bounds (its bytes
+  // only once the form is known: a workgroup that ends at once loads nothing).
+  const uint64_t bnd0 = in_off[0], bndn = in_off[n];
+  uint64_t L0 = (uint64_t)blockIdx.x * kT;
+  uint64_t L1 = min(L0 + (uint64_t)kT, n);
+  const uint64_t Ls = min(L0, n);
+  uint64_t i_cur = uniform64(vload(in_off, Ls)), o_cur = kEmit ? uniform64(vload(out_off, Ls)) : 0u;
+  uint64_t i_end = uniform64(vload(in_off, max(L1, Ls)));
+  if ((bndn - bnd0) > (uint64_t)kShortMean * n) {
+    if (blockIdx.x >= n_persist) return;
+    L0 = (uint64_t)blockIdx.x * per_block;
+    if (L0 >= n) return;
+    L1 = min(L0 + per_block, n);
+    i_cur = uniform64(vload(in_off, L0));
+    o_cur = kEmit ? uniform64(vload(out_off, L0)) : 0u;
+    i_end = uniform64(vload(in_off, L1));
+  } else if (L0 >= n) {
+    return;
+  }
   Next nx;
-  issue_next<kEmit>(nx, in, in_bias, in_off, out_off, cur, L1, i_cur, i_end, tid);
+  issue_next<kEmit>(nx, in, in_bias, in_off, out_off, L0, L1, i_cur, i_end, tid);
+  uint64_t cur = L0;
   for (uint32_t i = tid; i < 256u; i += kT) sm.code[i] = make_uint2(g_code[i], g_len[i]);
   uint8_t *pd_o = nullptr;  // the previous sub-tile's output, still in LDS
   uint32_t pd_lo = 0, pd_hi = 0;
@@ -537,9 +561,12 @@ hipError_t launch_encode_len(const DevTables &t, const uint8_t *in, const uint64
 hipError_t launch_encode(const DevTables &t, const uint8_t *in, const uint64_t *in_off, uint64_t in_bias,
                          uint64_t n, uint8_t *out, const uint64_t *out_off, uint64_t out_bias, hipStream_t s) {
   if (n == 0) return hipSuccess;
-  const unsigned grid = dev::tile_grid((n + kT - 1) / kT, 1, MHQ_ENC_BLOCKS * MHQ_PER_CU);
+  // persistent form: MHQ_ENC_BLOCKS resident workgroups per CU (never more than the tiles)
+  const unsigned persist = dev::tile_grid((n + kT - 1) / kT, 1, MHQ_ENC_BLOCKS * MHQ_PER_CU);
+  const uint64_t tiles = (n + kT - 1) / kT;
+  const unsigned grid = (unsigned)(tiles > persist ? tiles : persist);
   encode_kernel<true><<<dim3(grid), dim3(kT), 0, s>>>(in, in_off, in_bias, n, out, out_off, out_bias, nullptr, t.code,
-                                                       t.len, (n + grid - 1) / grid);
+                                                       t.len, (n + persist - 1) / persist, persist);
   return hipGetLastError();
 }
 
