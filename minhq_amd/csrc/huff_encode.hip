@@ -42,6 +42,9 @@
 #ifndef MHQ_ENC_BRANCHY  // 1: the bit writer ORs a word out under a per-code branch (0: branch free, config 4 -7 %, config 2 +10 %)
 #define MHQ_ENC_BRANCHY 1
 #endif
+#ifndef MHQ_LEN_U32ROW  // 1: encode_len writes P for every byte of a round as u32 (four 16-B stores per lane)
+#define MHQ_LEN_U32ROW 0
+#endif
 #ifndef MHQ_ENC_BLOCKS  // resident workgroups per CU
 #define MHQ_ENC_BLOCKS 3
 #endif
@@ -457,7 +460,15 @@ __global__ __launch_bounds__(kLenT) void encode_len_kernel(const uint8_t *__rest
   // dword): text lookups are nearly conflict-free, where a u32 table put
   // 0x21 / 0x41 / 0x61 on one bank
   __shared__ uint8_t lens[256];
+#if MHQ_LEN_U32ROW
   __shared__ uint32_t pw[kLenT / kWave][kRound + 4];  // P over one round (+ the position after it)
+#else
+  // P over one round as chunk prefixes (u32, + the position after the round)
+  // and in-chunk prefixes (u16, at most 15 x 30 bits): two 16-B stores per
+  // lane and round instead of four
+  __shared__ uint32_t ppre[kLenT / kWave][kWave + 4];
+  __shared__ __attribute__((aligned(16))) uint16_t pq[kLenT / kWave][kRound];
+#endif
   __shared__ uint64_t part[2 * (kLenT / kWave)];
   const uint32_t lane = threadIdx.x % kWave, wave = threadIdx.x / kWave;
   const uint64_t s = (uint64_t)blockIdx.x * kLenT + (uint64_t)wave * kWave;  // the wave's first literal
@@ -496,7 +507,12 @@ __global__ __launch_bounds__(kLenT) void encode_len_kernel(const uint8_t *__rest
       goto sums;
     }
     const uint32_t pa = (uint32_t)((uintptr_t)(in + a) - base), pb = (uint32_t)((uintptr_t)(in + b) - base);
+#if MHQ_LEN_U32ROW
     uint32_t *row = pw[wave];
+#else
+    uint32_t *pre_row = ppre[wave];
+    uint16_t *q_row = pq[wave];
+#endif
     uint32_t carry = 0, Pa = 0, Pb = 0;
     for (uint32_t r0 = 0; r0 < nround; r0 += kLenRB) {
       u32x4 v[kLenRB];
@@ -512,6 +528,7 @@ __global__ __launch_bounds__(kLenT) void encode_len_kernel(const uint8_t *__rest
         uint32_t q[16];
         const uint32_t tot = chunk_bits(v[k], lens, q);
         const uint32_t pre = carry + wave_incl_scan(tot) - tot;
+#if MHQ_LEN_U32ROW
 #pragma unroll
         for (int j = 0; j < 16; j += 4)
           *(u32x4 *)(row + prow(16u * lane + j)) = u32x4{pre + q[j], pre + q[j + 1], pre + q[j + 2], pre + q[j + 3]};
@@ -520,6 +537,23 @@ __global__ __launch_bounds__(kLenT) void encode_len_kernel(const uint8_t *__rest
         const uint32_t lo = (r0 + k) * kRound;  // positions [lo, lo + kRound] are in the row
         if (pa - lo <= kRound) Pa = row[prow(pa - lo)];
         if (pb - lo <= kRound) Pb = row[prow(pb - lo)];
+#else
+        // q packed two per dword: lane l's 32 bytes at 32 l (the 8 lanes of a
+        // 16-B store group cover 256 consecutive bytes: no bank conflict)
+        *(u32x4 *)(q_row + 16u * lane) =
+            u32x4{q[0] | q[1] << 16, q[2] | q[3] << 16, q[4] | q[5] << 16, q[6] | q[7] << 16};
+        *(u32x4 *)(q_row + 16u * lane + 8u) =
+            u32x4{q[8] | q[9] << 16, q[10] | q[11] << 16, q[12] | q[13] << 16, q[14] | q[15] << 16};
+        pre_row[lane] = pre;
+        if (lane == kWave - 1) pre_row[kWave] = pre + tot;  // the position after the round
+        wave_sync();
+        const uint32_t lo = (r0 + k) * kRound;  // positions [lo, lo + kRound]
+        const uint32_t xa = pa - lo, xb = pb - lo;
+        if (xa < kRound) Pa = pre_row[xa >> 4] + q_row[xa];
+        if (xa == kRound) Pa = pre_row[kWave];
+        if (xb < kRound) Pb = pre_row[xb >> 4] + q_row[xb];
+        if (xb == kRound) Pb = pre_row[kWave];
+#endif
         carry = __builtin_amdgcn_readlane(pre + tot, kWave - 1);
         wave_sync();
       }
