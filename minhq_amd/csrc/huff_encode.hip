@@ -538,20 +538,32 @@ __global__ __launch_bounds__(kLenT) void encode_len_kernel(const uint8_t *__rest
         if (pa - lo <= kRound) Pa = row[prow(pa - lo)];
         if (pb - lo <= kRound) Pb = row[prow(pb - lo)];
 #else
-        // q packed two per dword: lane l's 32 bytes at 32 l (the 8 lanes of a
-        // 16-B store group cover 256 consecutive bytes: no bank conflict)
-        *(u32x4 *)(q_row + 16u * lane) =
-            u32x4{q[0] | q[1] << 16, q[2] | q[3] << 16, q[4] | q[5] << 16, q[6] | q[7] << 16};
-        *(u32x4 *)(q_row + 16u * lane + 8u) =
-            u32x4{q[8] | q[9] << 16, q[10] | q[11] << 16, q[12] | q[13] << 16, q[14] | q[15] << 16};
+        // When every in-chunk prefix of the round fits a byte (chunks under
+        // 16 bits per byte: all text), q is stored as bytes, lane l's 16 at
+        // 16 l (one 16-B store; a store group's 8 lanes on 128 consecutive
+        // bytes); otherwise as u16, lane l's 32 bytes at 32 l (two stores, a
+        // group's lanes on 256 consecutive bytes).  No bank conflict either way.
+        const bool bytes = __ballot(q[15] > 255u) == 0;  // (uniform)
+        if (bytes) {
+          uint32_t d[4];
+#pragma unroll
+          for (int j = 0; j < 4; j++) d[j] = q[4 * j] | q[4 * j + 1] << 8 | q[4 * j + 2] << 16 | q[4 * j + 3] << 24;
+          *(u32x4 *)((uint8_t *)q_row + 16u * lane) = u32x4{d[0], d[1], d[2], d[3]};
+        } else {
+          *(u32x4 *)(q_row + 16u * lane) =
+              u32x4{q[0] | q[1] << 16, q[2] | q[3] << 16, q[4] | q[5] << 16, q[6] | q[7] << 16};
+          *(u32x4 *)(q_row + 16u * lane + 8u) =
+              u32x4{q[8] | q[9] << 16, q[10] | q[11] << 16, q[12] | q[13] << 16, q[14] | q[15] << 16};
+        }
         pre_row[lane] = pre;
         if (lane == kWave - 1) pre_row[kWave] = pre + tot;  // the position after the round
         wave_sync();
         const uint32_t lo = (r0 + k) * kRound;  // positions [lo, lo + kRound]
         const uint32_t xa = pa - lo, xb = pb - lo;
-        if (xa < kRound) Pa = pre_row[xa >> 4] + q_row[xa];
+        const uint8_t *q8 = (const uint8_t *)q_row;
+        if (xa < kRound) Pa = pre_row[xa >> 4] + (bytes ? (uint32_t)q8[xa] : (uint32_t)q_row[xa]);
         if (xa == kRound) Pa = pre_row[kWave];
-        if (xb < kRound) Pb = pre_row[xb >> 4] + q_row[xb];
+        if (xb < kRound) Pb = pre_row[xb >> 4] + (bytes ? (uint32_t)q8[xb] : (uint32_t)q_row[xb]);
         if (xb == kRound) Pb = pre_row[kWave];
 #endif
         carry = __builtin_amdgcn_readlane(pre + tot, kWave - 1);
