@@ -91,14 +91,15 @@ struct CapVal {  // in_off -> decode capacity floor(8*len/5)
   }
 };
 
-struct PairVal {  // two independent u32 lengths -> two offset arrays
+struct PairVal {  // two independent u32 lengths -> two offset arrays (b null: one, the other sums 0)
   const uint32_t *a, *b;  // 16-B aligned
   uint64_t n;
   __device__ inline void load(uint64_t i0, uint64_t *x, uint64_t *y) const {
     if (i0 + kItems <= n) {
 #pragma unroll
       for (int q = 0; q < kItems / 4; q++) {
-        const u32x4 u = ((const u32x4 *)(a + i0))[q], v = ((const u32x4 *)(b + i0))[q];
+        const u32x4 u = ((const u32x4 *)(a + i0))[q];
+        const u32x4 v = b ? ((const u32x4 *)(b + i0))[q] : u32x4{0u, 0u, 0u, 0u};
         x[4 * q] = u.x; x[4 * q + 1] = u.y; x[4 * q + 2] = u.z; x[4 * q + 3] = u.w;
         y[4 * q] = v.x; y[4 * q + 1] = v.y; y[4 * q + 2] = v.z; y[4 * q + 3] = v.w;
       }
@@ -106,7 +107,7 @@ struct PairVal {  // two independent u32 lengths -> two offset arrays
 #pragma unroll
       for (int k = 0; k < kItems; k++) {
         x[k] = i0 + k < n ? a[i0 + k] : 0u;
-        y[k] = i0 + k < n ? b[i0 + k] : 0u;
+        y[k] = b && i0 + k < n ? b[i0 + k] : 0u;
       }
     }
   }

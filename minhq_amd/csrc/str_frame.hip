@@ -539,7 +539,7 @@ hipError_t launch_read_strings(const DevTables &t, const uint8_t *blk, uint64_t 
                                              (uint64_t *)(base + L.sums));
   TRY(hipGetLastError());
   // output regions: capacities back to back
-  TRY(launch_offsets_pair_sums(sc.cap, sc.cap, n, (uint64_t *)(base + L.sums), out_cap, out_cap, out_off, nullptr,
+  TRY(launch_offsets_pair_sums(sc.cap, nullptr, n, (uint64_t *)(base + L.sums), out_cap, out_cap, out_off, nullptr,
                                s));
   TRY(launch_decode(t, blk, sc.start, 0, n, out, out_off, 0, out_len, status, s, sc.hend));
   read_finish_kernel<<<(unsigned)((n + kT * kParsePer - 1) / (kT * kParsePer)), kT, 0, s>>>(blk, sc, n, out_off, next, out, out_len, status, out_cap);
