@@ -290,7 +290,7 @@ __device__ __forceinline__ bool masked_step(const Smem &sm, uint32_t *otgt, BitB
 #endif
   const uint32_t w = in.next_word();
   bool lng = false;
-  if (e == 0u && !stop) {  // a code of 13..29 bits
+  if ((e == 0u) & !stop) {  // a code of 13..29 bits (one branch: no short circuit)
     uint32_t sym = 0;
     const uint32_t L = long_code(sm.lut2, S, sym);
     e = L | (8u << 8) | (sym << 16);
