@@ -59,6 +59,9 @@
 #ifndef MHQ_DEC_P3  // a third LUT1 probe per step of the masked loop
 #define MHQ_DEC_P3 0
 #endif
+#ifndef MHQ_DEC_LONG1  // 0: only the step before the end test resolves codes of 13+ bits
+#define MHQ_DEC_LONG1 0
+#endif
 #ifndef MHQ_DEC_STEPS  // masked steps per end test of the probe loop
 #define MHQ_DEC_STEPS 2
 #endif
@@ -280,6 +283,10 @@ struct BitBufM {
 struct Pend {
   uint32_t ow, v;
 };
+// kLong false (the steps before the end test): a code of 13+ bits is left
+// for the next step (its LUT1 entry is 0, so nothing is consumed: the step
+// only refills), which saves the LUT2 branch in those steps.
+template <bool kLong = true>
 __device__ __forceinline__ bool masked_step(const Smem &sm, uint32_t *otgt, BitBufM &in, OutAcc &out, Pend &pend,
                                             bool &stop) {
   const uint32_t S = in.top32();
@@ -290,7 +297,7 @@ __device__ __forceinline__ bool masked_step(const Smem &sm, uint32_t *otgt, BitB
 #endif
   const uint32_t w = in.next_word();
   bool lng = false;
-  if ((e == 0u) & !stop) {  // a code of 13..29 bits (one branch: no short circuit)
+  if (kLong && ((e == 0u) & !stop)) {  // a code of 13..29 bits (one branch: no short circuit)
     uint32_t sym = 0;
     const uint32_t L = long_code(sm.lut2, S, sym);
     e = L | (8u << 8) | (sym << 16);
@@ -658,7 +665,7 @@ __device__ __forceinline__ void decode_piece(const Smem &sm, WaveSmem &ws, uint3
       // consumed at the EOS prefix; `left` stays negative, the word held
       // back), so the last step's result covers them all
 #pragma unroll
-      for (int k = 1; k < MHQ_DEC_STEPS; k++) masked_step(sm, ws.out_w, in, out, pend, stop);
+      for (int k = 1; k < MHQ_DEC_STEPS; k++) masked_step<MHQ_DEC_LONG1 != 0>(sm, ws.out_w, in, out, pend, stop);
       if (masked_step(sm, ws.out_w, in, out, pend, stop)) {
         // stop: the EOS prefix at p (INVALID when a 31st bit of the literal follows)
         const uint32_t r = in.left < 0 ? kRedo : (out.optr() - ost) | ((uint32_t)(in.left > kEosOnes) << 31);
