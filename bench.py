@@ -73,11 +73,12 @@ def spawn_ranks(n: int) -> int:
     return subprocess.call(cmd, env=env)
 
 
-# Rehearsal knobs for the N > 1 path on a box with fewer GPUs than ranks (the
-# driver's multi-GPU runs set neither): MHQ_BENCH_BACKEND=gloo keeps the
-# barriers and the max-over-ranks on the CPU, MHQ_BENCH_SHARE_GPU=1 maps rank
-# r to GPU r mod (GPUs visible).
-BACKEND = os.environ.get("MHQ_BENCH_BACKEND", "nccl")
+# The process group only carries barriers and one max over ranks (the path has
+# no data exchange), so it runs on gloo over the host: an RCCL
+# communicator would be initialised on every rank for a handful of scalars.
+# MHQ_BENCH_BACKEND=nccl selects RCCL instead; MHQ_BENCH_SHARE_GPU=1 maps rank
+# r to GPU r mod (GPUs visible), to rehearse N > 1 on fewer GPUs.
+BACKEND = os.environ.get("MHQ_BENCH_BACKEND", "gloo")
 
 
 def dist_setup():
@@ -287,10 +288,10 @@ def cpu_baseline(batch, seconds: float):
 class Dev:
     """Device-resident copies of one batch and its encoded form."""
 
-    def __init__(self, codec, data, off, dev):
+    def __init__(self, codec, data, off, dev, encode=True):
         import torch
 
-        self.data, self.off = data, off
+        self.codec, self.data, self.off = codec, data, off
         n = off.numel() - 1
         self.n = n
         self.plain = int((off[-1] - off[0]).item())
@@ -302,7 +303,16 @@ class Dev:
         self.enc_bytes = int(self.enc_off[-1].item())
         self.cap_bytes = int(self.cap_off[-1].item())
         self.enc = torch.empty(self.enc_bytes + 16, dtype=torch.uint8, device=dev)
-        codec.encode_dev(data, off, self.enc, self.enc_off)
+        if encode:
+            self.encode_range(0, n)
+
+    def encode_range(self, lo, hi):
+        """Encodes literals [lo, hi) into their place in self.enc (a rank
+        encodes only the shard it decodes)."""
+        import torch
+
+        if hi > lo:
+            self.codec.encode_dev(self.data, self.off[lo:hi + 1], self.enc, self.enc_off[lo:hi + 1])
         torch.cuda.synchronize()
 
 
@@ -355,10 +365,13 @@ def config4_sharded(codec, dev, world, rank, pg, launches, rotate_bytes):
     from minhq_amd import shard, workloads
 
     n = 1 << 24
+    # every rank builds the batch's layout (encode_len + scan: the shard plan
+    # splits by encoded bytes) but encodes only the shard it decodes
     data, off = workloads.make_batch_device(n, "zipf", "hdr", workloads.SEED_ZIPF, device=dev)
-    dv = Dev(codec, data, off, dev)
+    dv = Dev(codec, data, off, dev, encode=False)
     parts = shard.plan_shards_device(dv.enc_off, world)
     lo, hi = parts[rank]
+    dv.encode_range(lo, hi)
     slots = decode_slots(dv, lo, hi, rotate_bytes, dev)
 
     def run(i):

@@ -155,7 +155,8 @@ int mhq_read_strings_dev(mhq_ctx *ctx, int dev, const uint8_t *blk, uint64_t blk
  * status[i] (MHQ_STR_OK, or MHQ_STR_NOSPACE past out_cap).  With out NULL only
  * out_off is computed (size query).  Device pointers; asynchronous on `stream`
  * (no synchronisation inside: only payloads whose frames fit out_cap are
- * encoded, into scratch sized from out_cap). */
+ * encoded, into device scratch of about out_cap bytes -- kept per stream up
+ * to 64 MiB, taken in stream order for the call above that). */
 int mhq_write_strings_dev(mhq_ctx *ctx, int dev, const uint8_t *in, const uint64_t *in_off, uint64_t n,
                           const uint8_t *prefix, const uint8_t *lead, int choice, uint8_t *out, uint64_t out_cap,
                           uint64_t *out_off, uint8_t *status, void *stream);

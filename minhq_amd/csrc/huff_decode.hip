@@ -538,12 +538,15 @@ struct TileIn {
 // flight and is then overwritten makes the compiler wait for the load).
 __device__ __forceinline__ void load_in(TileIn &t, const uint8_t *__restrict__ in, uint64_t in_bias, uint64_t ib,
                                         uint64_t iend, uint32_t lane, uint32_t *keep = nullptr) {
+  // (nothing for an empty or reversed range: literals out of order -- the
+  // framed strings of read_strings may be -- give iend < ib, and such a tile
+  // is never staged; loading from ib would read past the buffer's end)
+  if (iend <= ib) return;
   const uint8_t *a = in + (ib - in_bias);
   const uint32_t delta = (uint32_t)((uintptr_t)a & 15u);
   const u32x4 *src = (const u32x4 *)(a - delta);
   const uint64_t need = ((iend - ib) + delta + 15u) >> 4;
   const uint32_t chunks = (uint32_t)min(need, (uint64_t)(kWIn / 16));
-  if (iend == ib) return;
 #pragma unroll
   for (int k = 0; k < kPF; k++) {
     const uint32_t c = min(lane + (uint32_t)kWave * k, chunks - 1u);
@@ -1209,9 +1212,6 @@ hipError_t launch_decode(const DevTables &t, const uint8_t *in, const uint64_t *
                          uint64_t n, uint8_t *out, const uint64_t *out_off, uint64_t out_bias,
                          uint32_t *out_len, uint8_t *status, hipStream_t s, const uint64_t *in_end) {
   if (n == 0) return hipSuccess;
-#ifdef MHQ_DEC_WG
-  if (!in_end) return launch_decode_wg(t, in, in_off, in_bias, n, out, out_off, out_bias, out_len, status, s);
-#endif
   // One workgroup per CU, each a contiguous range of whole wave tiles.  The
   // tile length (<= kTile) is chosen so that every wave gets the same number
   // of tiles: no wave idles through a last, partial round.  (A shorter first

@@ -42,10 +42,6 @@ hipError_t launch_decode(const DevTables &t, const uint8_t *in, const uint64_t *
                          uint64_t in_bias, uint64_t n, uint8_t *out, const uint64_t *out_off,
                          uint64_t out_bias, uint32_t *out_len, uint8_t *status, hipStream_t s,
                          const uint64_t *in_end = nullptr);
-// The workgroup-cooperative decode (huff_decode_wg.hip); same contract.
-hipError_t launch_decode_wg(const DevTables &t, const uint8_t *in, const uint64_t *in_off,
-                            uint64_t in_bias, uint64_t n, uint8_t *out, const uint64_t *out_off,
-                            uint64_t out_bias, uint32_t *out_len, uint8_t *status, hipStream_t s);
 // out_off[i] = base + sum_{j<i} enc_len[j]; cap_off[i] = base + sum_{j<i} floor(8*enc_len[j]/5)
 // (either output may be null).  Scratch: offsets_scratch_bytes(n) bytes, or
 // null for a hipMallocAsync on `s`.

@@ -86,15 +86,25 @@ struct Device {
     hipStream_t s;
     void *p;
     size_t bytes;
+    int holders;  // callers between stream_scratch and the end of their enqueueing (ScratchLease)
   };
   std::mutex scratch_mu;
   std::vector<Scratch> scratch;
-  // Buffers a stream outgrew.  Work already queued (possibly by another
-  // thread on the same stream) may still use them, so they are freed only at
-  // mhq_close, never while a caller can hold their pointer.
-  std::vector<void *> retired;
+  // Buffers a stream outgrew.  Work queued (possibly by another thread on the
+  // same stream) may still use them: once the last caller holding one has
+  // finished enqueueing (its ScratchLease ends) an event is recorded on the
+  // stream, and the buffer is freed when that event has completed (checked
+  // whenever a scratch buffer is handed out), or at mhq_close.
+  struct Retired {
+    void *p;
+    hipStream_t s;
+    int holders;
+    hipEvent_t done;  // recorded once holders reaches 0 (null before)
+  };
+  std::vector<Retired> retired;
 };
 constexpr size_t kMaxScratchStreams = 64;
+constexpr size_t kMaxCachedWriteScratch = (size_t)64 << 20;
 
 }  // namespace
 
@@ -157,8 +167,24 @@ void free_device(Device *d) {
   if (d->table_mem) (void)hipFree(d->table_mem);
   for (auto &x : d->scratch) (void)hipFree(x.p);
   d->scratch.clear();
-  for (void *p : d->retired) (void)hipFree(p);
+  for (auto &r : d->retired) {
+    (void)hipFree(r.p);
+    if (r.done) (void)hipEventDestroy(r.done);
+  }
   d->retired.clear();
+}
+
+// Records the event after which a retired buffer may be freed (no holder is
+// left, so every use of it is already on the stream).  Under scratch_mu.
+void mark_retired(Device::Retired &r) {
+  if (r.holders > 0 || r.done) return;
+  hipEvent_t ev = nullptr;
+  if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) return;  // kept until mhq_close
+  if (hipEventRecord(ev, r.s) != hipSuccess) {
+    (void)hipEventDestroy(ev);
+    return;
+  }
+  r.done = ev;
 }
 
 // The scratch buffer of stream s, at least `bytes` long, or null when the
@@ -168,16 +194,33 @@ void free_device(Device *d) {
 // have just been handed it for work it is still queueing on the same stream.
 void *stream_scratch(Device *d, hipStream_t s, size_t bytes) {
   std::lock_guard<std::mutex> g(d->scratch_mu);
+  // free the retired buffers whose stream has passed its last use
+  for (size_t i = 0; i < d->retired.size();) {
+    Device::Retired &r = d->retired[i];
+    if (r.done && hipEventQuery(r.done) == hipSuccess) {
+      (void)hipFree(r.p);
+      (void)hipEventDestroy(r.done);
+      r = d->retired.back();
+      d->retired.pop_back();
+    } else {
+      i++;
+    }
+  }
   for (auto &x : d->scratch) {
     if (x.s != s) continue;
-    if (x.bytes >= bytes) return x.p;
+    if (x.bytes >= bytes) {
+      x.holders++;
+      return x.p;
+    }
     size_t b = 1;
     while (b < bytes) b <<= 1;
     void *p = nullptr;
     if (hipMalloc(&p, b) != hipSuccess) return nullptr;
-    d->retired.push_back(x.p);
+    d->retired.push_back(Device::Retired{x.p, s, x.holders, nullptr});
+    mark_retired(d->retired.back());
     x.p = p;
     x.bytes = b;
+    x.holders = 1;
     return x.p;
   }
   if (d->scratch.size() >= kMaxScratchStreams) return nullptr;
@@ -185,9 +228,37 @@ void *stream_scratch(Device *d, hipStream_t s, size_t bytes) {
   while (b < bytes) b <<= 1;
   void *p = nullptr;
   if (hipMalloc(&p, b) != hipSuccess) return nullptr;
-  d->scratch.push_back(Device::Scratch{s, p, b});
+  d->scratch.push_back(Device::Scratch{s, p, b, 1});
   return p;
 }
+
+// Ends a caller's hold on a buffer from stream_scratch (after it has
+// enqueued every use of it).
+void release_scratch(Device *d, void *p) {
+  if (!p) return;
+  std::lock_guard<std::mutex> g(d->scratch_mu);
+  for (auto &x : d->scratch)
+    if (x.p == p) {
+      x.holders--;
+      return;
+    }
+  for (auto &r : d->retired)
+    if (r.p == p) {
+      r.holders--;
+      mark_retired(r);
+      return;
+    }
+}
+
+// stream_scratch for the lifetime of one ABI call.
+struct ScratchLease {
+  Device *d;
+  void *p;
+  ScratchLease(Device *d_, hipStream_t s, size_t bytes) : d(d_), p(bytes ? stream_scratch(d_, s, bytes) : nullptr) {}
+  ~ScratchLease() { release_scratch(d, p); }
+  ScratchLease(const ScratchLease &) = delete;
+  ScratchLease &operator=(const ScratchLease &) = delete;
+};
 
 Device *device(mhq_ctx *ctx, int dev) {
   if (!ctx || dev < 0 || dev >= (int)ctx->devs.size()) return nullptr;
@@ -237,10 +308,13 @@ int run_chunk(Device *d, Stage &S, const HostJob &j, uint64_t a, uint64_t b) {
   const uint64_t out_bias = j.out_off[a];
   const uint64_t out_bytes = j.out_off[b] - j.out_off[a];
   MHQ_TRY(hipMemcpyAsync(S.out_off.p, j.out_off + a, (m + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, s));
-  // No fill of the staging region: bytes past out_len / enc_len are
-  // unspecified (include/mhq_huff.h), and whatever the kernels leave there is
-  // copied back as is.
+  // The staging region is zeroed first: the region is copied back whole, and
+  // bytes the kernels leave alone (past a literal's out_len on the decode's
+  // streamed path) would otherwise carry an earlier call's data into the
+  // caller's buffer.  (A device-side fill of at most a few MB per chunk,
+  // hidden behind the chunk's copies.)
   uint8_t *dout = (uint8_t *)S.out.p;
+  MHQ_TRY(hipMemsetAsync(dout, 0, out_bytes, s));
   const uint64_t *dout_off = (const uint64_t *)S.out_off.p;
   if (j.op == Op::kEncode) {
     MHQ_TRY(mhq::launch_encode(d->tables, din, din_off, in_bias, m, dout, dout_off, out_bias, s));
@@ -413,8 +487,8 @@ int mhq_huff_offsets_dev(mhq_ctx *ctx, int dev, const uint32_t *enc_len, uint64_
   if (!d || !out_off || (n && !enc_len)) return MHQ_EINVAL;
   MHQ_TRY(hipSetDevice(d->ordinal));
   hipStream_t s = (hipStream_t)stream;
-  void *scratch = stream_scratch(d, s, mhq::offsets_scratch_bytes(n));
-  return hip_rc(mhq::launch_offsets(enc_len, n, base, out_off, cap_off, s, scratch));
+  ScratchLease scratch(d, s, mhq::offsets_scratch_bytes(n));
+  return hip_rc(mhq::launch_offsets(enc_len, n, base, out_off, cap_off, s, scratch.p));
 }
 
 int mhq_huff_encode_layout_dev(mhq_ctx *ctx, int dev, const uint8_t *in, const uint64_t *in_off, uint64_t n,
@@ -425,7 +499,8 @@ int mhq_huff_encode_layout_dev(mhq_ctx *ctx, int dev, const uint8_t *in, const u
   MHQ_TRY(hipSetDevice(d->ordinal));
   hipStream_t s = (hipStream_t)stream;
   const size_t bytes = mhq::offsets_sums_scratch_bytes(n);
-  uint64_t *sums = (uint64_t *)stream_scratch(d, s, bytes);
+  ScratchLease lease(d, s, bytes);
+  uint64_t *sums = (uint64_t *)lease.p;
   const bool own = sums == nullptr;
   if (own) MHQ_TRY(hipMallocAsync((void **)&sums, bytes, s));
   hipError_t e = mhq::launch_encode_len(d->tables, in, in_off, 0, n, enc_len, s, sums);
@@ -470,7 +545,8 @@ int mhq_read_strings_dev(mhq_ctx *ctx, int dev, const uint8_t *blk, uint64_t blk
   MHQ_TRY(hipSetDevice(d->ordinal));
   hipStream_t s = (hipStream_t)stream;
   // the stream's cached scratch (null: the launcher allocates in stream order)
-  void *scratch = n ? stream_scratch(d, s, mhq::read_strings_scratch_bytes(n, blk_len)) : nullptr;
+  ScratchLease lease(d, s, n ? mhq::read_strings_scratch_bytes(n, blk_len) : 0);
+  void *scratch = n ? lease.p : nullptr;
   return hip_rc(mhq::launch_read_strings(d->tables, blk, blk_len, pos, limit, prefix, n, out, out_cap, out_off,
                                          out_len, status, next, s, scratch));
 }
@@ -483,7 +559,14 @@ int mhq_write_strings_dev(mhq_ctx *ctx, int dev, const uint8_t *in, const uint64
   if (n && (!in_off || !prefix || !lead || (out && !status))) return MHQ_EINVAL;
   MHQ_TRY(hipSetDevice(d->ordinal));
   hipStream_t s = (hipStream_t)stream;
-  void *scratch = n ? stream_scratch(d, s, mhq::write_strings_scratch_bytes(n, out ? out_cap : 0)) : nullptr;
+  // The scratch holds the packed Huffman payloads, bounded only by out_cap (no
+  // size comes back to the host).  A scratch above kMaxCachedWriteScratch is
+  // taken in stream order for this call (hipMallocAsync / hipFreeAsync)
+  // rather than kept by the per-stream cache: a caller sizing out_cap for the
+  // worst case must not pin that much device memory until mhq_close.
+  const size_t want = mhq::write_strings_scratch_bytes(n, out ? out_cap : 0);
+  ScratchLease lease(d, s, n && want <= kMaxCachedWriteScratch ? want : 0);
+  void *scratch = n && want <= kMaxCachedWriteScratch ? lease.p : nullptr;
   return hip_rc(mhq::launch_write_strings(d->tables, in, in_off, n, prefix, lead, (uint32_t)choice, out, out_cap,
                                           out_off, status, s, scratch));
 }

@@ -94,6 +94,10 @@ __global__ __launch_bounds__(kT) void read_parse_kernel(const uint8_t *__restric
         take = v < avail ? v : avail;
       }
     }
+    // the decode reads literal i from blk + start: a header-error string's
+    // pos may lie anywhere (even past the block), so its (empty) payload is
+    // placed at min(pos, blk_len) -- every start stays inside [0, blk_len]
+    start = start < blk_len ? start : blk_len;
     sc.start[i] = start;
     sc.hend[i] = kind == 1 ? start + take : start;
     if (i == n - 1) sc.start[n] = blk_len;

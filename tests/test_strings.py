@@ -224,3 +224,52 @@ def test_read_gaps_full_tiles(codec, oracle_mod):
         assert (vals[i], int(st[i])) == (ref, _oracle_status(rc)), i
         assert int(nxt[i]) == pos[i] + used
     assert (np.asarray(st) == OK).all()
+
+
+def test_read_wild_pos_and_reverse_order_at_buffer_end(codec, oracle_mod):
+    """strings read in reverse block order and header-error
+    strings whose pos lies far past the block, with the block ending exactly
+    at the end of a 2 MiB device allocation.  The decode must never load from
+    blk + pos of an unreadable string, nor prefetch a tile from a reversed
+    range; every string against the oracle's ReadString."""
+    import numpy as np
+    import torch
+
+    rng = random.Random(41)
+    strs = _random_strings(rng, 3000)
+    blk = b"".join(oracle_mod.write_string(s, prefix=7, choice=1) for s in strs)
+    pos, p = [], 0
+    for s in strs:
+        pos.append(p)
+        p += len(oracle_mod.write_string(s, prefix=7, choice=1))
+    L = len(blk)
+    wild = [L, L + 3, L + 4096, 1 << 33, (1 << 62) + 5]
+    P = list(reversed(pos))
+    for k, w in enumerate(wild):  # scattered through the reversed run
+        P.insert(37 * (k + 1) % len(P), w)
+    n = len(P)
+    dev = torch.device("cuda:0")
+    whole = torch.zeros(2 << 20, dtype=torch.uint8, device=dev)
+    t_blk = whole[(2 << 20) - L:]
+    t_blk.copy_(torch.frombuffer(bytearray(blk), dtype=torch.uint8).to(dev))
+    t_pos = torch.tensor(np.asarray(P, dtype=np.uint64).view(np.int64), device=dev)
+    t_lim = torch.full((n,), L, dtype=torch.int64, device=dev)
+    t_pf = torch.full((n,), 7, dtype=torch.uint8, device=dev)
+    cap = L * 8 // 5 + 16
+    out = torch.zeros(cap, dtype=torch.uint8, device=dev)
+    out_off = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+    out_len = torch.zeros(n, dtype=torch.int32, device=dev)
+    st = torch.zeros(n, dtype=torch.uint8, device=dev)
+    nxt = torch.zeros(n, dtype=torch.int64, device=dev)
+    codec.read_strings_dev(t_blk, t_pos, t_lim, t_pf, out, out_off, out_len, st, nxt)
+    torch.cuda.synchronize()
+    o = out.cpu().numpy()
+    oo = out_off.cpu().numpy().view(np.uint64)
+    ol = out_len.cpu().numpy()
+    s_h = st.cpu().numpy()
+    nx = nxt.cpu().numpy().view(np.uint64)
+    for k, q in enumerate(P):
+        ref, rc, used = oracle_mod.read_string(blk[q:] if q < L else b"", prefix=7)
+        got = o[int(oo[k]): int(oo[k]) + int(ol[k])].tobytes()
+        assert (got, int(s_h[k])) == (ref, _oracle_status(rc)), (k, q)
+        assert int(nx[k]) == q + used, (k, q)
