@@ -65,6 +65,9 @@
 #ifndef MHQ_DEC_STEPS  // masked steps per end test of the probe loop
 #define MHQ_DEC_STEPS 2
 #endif
+#ifndef MHQ_DEC_SOPEN  // 1: the first tile's input loads are addressed by two scalar loads (no wait for the offsets)
+#define MHQ_DEC_SOPEN 0
+#endif
 #ifndef MHQ_DEC_WOUT  // a wave's output slice (bytes, multiple of 16)
 #define MHQ_DEC_WOUT 6448
 #endif
@@ -1049,10 +1052,23 @@ __global__ __launch_bounds__(kT) void decode_kernel(const uint8_t *__restrict__ 
   // (Every wave loads them, as scalar loads, and waits for them only where
   // they are used: a load under `tid == 0` waited at once.)
   const uint64_t bnd[4] = {in_off[n], in_off[0], out_off[n], out_off[0]};
+#if MHQ_DEC_SOPEN
+  // The first tile's input range comes from two scalar loads (the tile's first
+  // and one-past-last literal), so its input loads are issued without waiting
+  // for the per-lane offsets, which load alongside.
+  const uint64_t s0 = L0 + (uint64_t)__builtin_amdgcn_readfirstlane(tile) * tl0;
+  const uint64_t ib0 = in_off[min(s0, L1)], ie0 = in_off[min(s0 + (uint64_t)tl0, L1)];
+  TileIn tin;
+  uint32_t keep[kPF] = {};
+  load_in(tin, in, in_bias, ib0, ie0, lane, keep);
+  load_off_in<kGaps>(off, in_off, in_end, L0 + (uint64_t)tile * tl0, L1, tl0, lane);
+#else
   load_off_in<kGaps>(off, in_off, in_end, L0 + (uint64_t)tile * tl0, L1, tl0, lane);
   TileIn tin;
   uint32_t keep[kPF] = {};
   load_in(tin, in, in_bias, uniform64(off.i0), uniform64(off.ie), lane, keep);
+#endif
+  TL(56);  // the first tile's input loads issued
   load_off_out(off, out_off, L0 + (uint64_t)tile * tl0, L1, tl0, lane);
   static_assert(kLut1Size / 4 <= 2 * kT && kLut2Size / 8 <= kT && kT >= 64, "table copy shape");
   // (loads and stores from clamped indices, none under a branch: a load
@@ -1085,6 +1101,7 @@ __global__ __launch_bounds__(kT) void decode_kernel(const uint8_t *__restrict__ 
   __syncthreads();
 #pragma unroll
   for (int k = 0; k < kPF; k++) asm volatile("" ::"v"(keep[k]));
+  TL(57);  // tables in LDS
   const uint32_t tl = __builtin_amdgcn_readfirstlane(sm.tl);
   if (tl != tl0) {  // the loads above used tl0: again with tl
     load_off<kGaps>(off, in_off, in_end, out_off, L0 + (uint64_t)tile * tl, L1, tl, lane);
@@ -1135,6 +1152,7 @@ __global__ __launch_bounds__(kT) void decode_kernel(const uint8_t *__restrict__ 
       if (j0 < cnt) ws.rec[j0] = (uint32_t)(off.i0 - ib + idelta) | (uint32_t)(off.o0 - ob + odelta) << 16;
       if (j0 + 1u < cnt) ws.rec[j0 + 1] = (off.i1 - (uint32_t)ib + idelta) | (off.o1 - (uint32_t)ob + odelta) << 16;
       if (lane == 0) ws.rec[cnt] = (uint32_t)(ie - ib + idelta) | (uint32_t)(oe - ob + odelta) << 16;
+      if (tl_j == 0) TL(58);  // the first tile's input and output offsets arrived
     }
     // the next tile's input (its offsets arrived during the previous decode), the offsets of the one after
     load_in(tin, in, in_bias, uniform64(off2.i0), uniform64(off2.ie), lane);

@@ -89,6 +89,11 @@ def timeline_report(fn):
                 cols.append(f"g{g}: issued@{us(x[:, b]).mean():.1f} sorted@{us(x[:, b + 2]).mean():.1f} "
                             f"loop {(x[:, b + 3] - x[:, b + 2]).mean() / 100:.2f} done@{us(x[:, b + 4]).mean():.1f}")
         print(f"  tile {j} by age group: " + " | ".join(cols), file=sys.stderr)
+    for slot, what in ((56, "first offsets in"), (57, "tables in LDS"), (58, "first input staged")):
+        ok = a[:, slot] > 0
+        if ok.any():
+            print(f"  opening: {what} @{us(a[ok, slot]).mean():.2f} us (p90 {np.percentile(us(a[ok, slot]), 90):.2f})",
+                  file=sys.stderr)
     print(f"timeline: {a.shape[0]} waves, start spread {us(a[:, 0]).max():.2f} us, end max {end.max():.2f} "
           f"p50 {np.percentile(end, 50):.2f} p10 {np.percentile(end, 10):.2f} us", file=sys.stderr)
     prev = a[:, 0]
