@@ -597,21 +597,22 @@ sums:
 }
 
 // ---- wave-cooperative encode ----------------------------------------------
-// A wave takes 64 consecutive literals and walks their whole byte range in
-// rounds of 1 KiB, lane l on aligned 16-B chunk l of the round (one coalesced
-// load per lane, every byte loaded once), as encode_len does.  No lane owns a
-// literal; where a code goes follows from the output layout itself:
+// A wave takes K groups of 64 consecutive literals (64 K literals) and walks
+// their whole byte range in rounds of 1 KiB, lane l on aligned 16-B chunk l of
+// the round (one coalesced load per lane, every byte loaded once), as
+// encode_len does.  No lane owns a literal; where a code goes follows from the
+// output layout itself:
 //   * a literal's first code starts at bit 8 * out_off[i] (relative to the
-//     wave's 16-B aligned output base): the literal lanes write that position
-//     into the round's qtab at the literal's first byte and set the byte's
-//     bit in the round's start mask;
+//     wave's 16-B aligned output base, plus kPB): the lane holding the literal
+//     writes that position into the round's qtab at the literal's first byte
+//     (zero = no literal starts at that byte);
 //   * every other code starts where the previous byte's code ended.  So the
 //     position of a chunk's first byte is a segmented scan over the lanes:
 //     each lane's chunk sums up to (starts in it?, end position) -- its last
 //     start's position plus the code lengths after it, or the sum of all its
 //     lengths -- and the wave combines them (a start resets the sum) in one
 //     DPP scan, carried from round to round;
-//   * each lane then places its 16 codes into a 64-bit accumulator and ORs
+//   * each lane then places its 16 codes through a two-word window and ORs
 //     complete words into the wave's LDS output ring.
 // The ring holds the complement of the output (the table's codes are stored
 // complemented, bits a code does not cover stay 0), so the padding after a
@@ -620,34 +621,36 @@ sums:
 // inverted.  After each round the complete 16-B chunks of the ring leave as
 // aligned stores (bytes of the chunks at the wave's two ends that belong to a
 // neighbour's region are left alone).
+// Bytes that belong to no literal of the wave cost nothing extra: positions
+// start kPB bits before the region, so the bytes before the first literal (in
+// the first chunk) are placed there, before the first literal's start resets
+// the position; the range's end is one more start (at the region's end), so
+// the bytes after it land past the region; chunks past the range read as '0'
+// (5-bit codes) and land past it too.  Nothing outside [region start, region
+// end) is ever stored.
 // Waves whose layout the ring cannot express (a literal with an empty output
 // region -- the caller skips it -- or offsets out of order, or more than
-// 2^27 bytes) encode one literal per lane from global memory instead.
+// 2^27 bytes, or a round whose output would overflow the ring: regions much
+// longer than their codes) encode one literal per lane from global memory.
 #ifndef MHQ_ENC_COOP  // 1: the wave-cooperative encode; 0: one thread per literal (encode_kernel)
 #define MHQ_ENC_COOP 1
 #endif
-#ifndef MHQ_ENC_DIRECT  // 1: every code ORed straight into the ring (two words); 0: a 64-bit window per lane
-#define MHQ_ENC_DIRECT 0
-#endif
-#ifndef MHQ_ENC_EMIT1  // 1: the first word out of the window as a plain branch
-#define MHQ_ENC_EMIT1 0
+#ifndef MHQ_ENC_X  // timing experiments only (wrong output): 1 no table lookups, 2 no ring ORs in pass 2, 4 no qtab reads
+#define MHQ_ENC_X 0
 #endif
 #ifndef MHQ_ENC_K  // literal groups of 64 per wave (0: by batch size)
 #define MHQ_ENC_K 0
 #endif
-constexpr int kCT = 256;                      // threads per workgroup: 4 waves
+constexpr int kCT = 256;          // threads per workgroup: 4 waves
 constexpr int kCW = kCT / kWave;
-constexpr uint32_t kRingW = 1024;             // output ring words per wave (4 KiB; a round writes < 990)
-constexpr uint32_t kDeadEntry = 256;          // code table entry of length 0 (bytes outside the range)
+constexpr uint32_t kRingW = 1024;  // output ring words per wave (4 KiB)
+constexpr uint32_t kPB = 512;      // bit positions start 64 bytes before the wave's output base
+constexpr uint32_t kZeroBytes = 0x30303030u;  // '0' x 4: 5-bit codes for chunks past the range
 
 struct CoopSmem {
-  uint2 code[260];                     // (complemented code bits, length); [256]: (0, 0)
-  // complemented output words (MSB-first values), zero where unwritten; word
-  // kRingW takes the second half of a code that crosses from slot kRingW-1
-  // into slot 0 (the flush of slot 0 merges it)
-  uint32_t ring[kCW][kRingW + 4];
-  uint32_t qtab[kCW][kRound];          // (prow) output bit position of a literal starting at a byte
-  uint32_t smask[kCW][kRound / 32 + 2];  // literal starts in the round, a bit per byte
+  uint2 code[256];                 // (complemented code, left-aligned; length)
+  uint32_t ring[kCW][kRingW];      // complemented output words (MSB-first values), zero where unwritten
+  uint32_t qtab[kCW][kRound];      // (prow) output bit position of a literal starting at a byte; 0: none
 };
 
 // Segmented inclusive scan of x = value | flag << 31 over the wave (lane order):
@@ -680,19 +683,31 @@ __device__ __forceinline__ uint64_t from_next_lane(uint64_t v, uint64_t last) {
 }
 
 // One literal by one lane straight from global memory (the fallback waves),
-// from the complemented table.
+// from the complemented, left-aligned table.
 __device__ void encode_literal_coop_global(const uint8_t *src, uint64_t nbytes, uint8_t *dst, const uint2 *code) {
   BitOutGlobal bo{dst, 0, 0};
   for (uint64_t i = 0; i < nbytes; i++) {
     const uint2 c = code[src[i]];
-#if MHQ_ENC_DIRECT
-    bo.put(c.y ? ~(c.x >> (32u - c.y)) & ((1u << c.y) - 1u) : 0u, c.y);
-#else
-    bo.put(~c.x & ((1u << c.y) - 1u), c.y);
-#endif
+    bo.put(~(c.x >> (32u - c.y)) & ((1u << c.y) - 1u), c.y);
   }
   bo.finish();
 }
+
+#ifdef MHQ_DIAG_ETL  // diagnostic build: per-wave timeline of the coop encode (s_memrealtime, 100 MHz)
+constexpr int kEtlSlots = 64;  // [0] start, [1] table ready, [2] offsets used, [3] first loads issued, [4 + r] round r done, [63] end
+constexpr int kEtlWaves = 16384;
+__device__ unsigned long long g_etl[kEtlWaves * kEtlSlots];
+#define ETL(slot)                                                                                    \
+  do {                                                                                               \
+    const uint32_t _w = blockIdx.x * kCW + threadIdx.x / kWave;                                      \
+    const int _s = (slot);                                                                           \
+    if (threadIdx.x % kWave == 0 && _w < kEtlWaves && _s < kEtlSlots) g_etl[_w * kEtlSlots + _s] = wall_clock64(); \
+  } while (0)
+#else
+#define ETL(slot) \
+  do {            \
+  } while (0)
+#endif
 
 template <int K>
 __global__ __launch_bounds__(kCT) void encode_coop_kernel(const uint8_t *__restrict__ in,
@@ -703,6 +718,7 @@ __global__ __launch_bounds__(kCT) void encode_coop_kernel(const uint8_t *__restr
                                                           const uint8_t *__restrict__ g_len) {
   __shared__ CoopSmem sm;
   const uint32_t tid = threadIdx.x, lane = tid % kWave, wave = tid / kWave;
+  ETL(0);
   // the wave's literals: K groups of 64, [s, s + 64 K); their offsets are
   // requested first so that the loads overlap the table set-up
   const uint64_t s = ((uint64_t)blockIdx.x * kCW + wave) * (uint64_t)(kWave * K);
@@ -718,21 +734,17 @@ __global__ __launch_bounds__(kCT) void encode_coop_kernel(const uint8_t *__restr
   {
     const uint32_t L = g_len[tid];
     const uint32_t c = ~g_code[tid] & ((1u << L) - 1u);
-#if MHQ_ENC_DIRECT
-    sm.code[tid] = make_uint2(L ? c << (32u - L) : 0u, L);  // left-aligned
-#else
-    sm.code[tid] = make_uint2(c, L);
-#endif
-    if (tid < 4) sm.code[kDeadEntry + tid] = make_uint2(0u, 0u);
+    sm.code[tid] = make_uint2(c << (32u - L), L);  // left-aligned (every length is 5..30)
   }
   uint32_t *ring = sm.ring[wave];
   uint32_t *qtab = sm.qtab[wave];
-  uint32_t *smask = sm.smask[wave];
 #pragma unroll
-  for (int k = 0; k < 4; k++) ((u32x4 *)ring)[lane + kWave * k] = u32x4{0u, 0u, 0u, 0u};
-  if (lane == 0) ((u32x4 *)ring)[kRingW / 4] = u32x4{0u, 0u, 0u, 0u};
-  if (lane < kRound / 32 + 2) smask[lane] = 0;
+  for (int k = 0; k < 4; k++) {
+    ((u32x4 *)ring)[lane + kWave * k] = u32x4{0u, 0u, 0u, 0u};
+    ((u32x4 *)qtab)[lane + kWave * k] = u32x4{0u, 0u, 0u, 0u};
+  }
   __syncthreads();  // the code table; the waves are independent from here on
+  ETL(1);
   if (s >= n) return;
   const uint64_t A = uniform64(a[0]), OA = uniform64(o[0]);
   // layouts the ring cannot express: a literal whose output region is empty
@@ -751,233 +763,216 @@ __global__ __launch_bounds__(kCT) void encode_coop_kernel(const uint8_t *__restr
     nonempty[k] = valid && b[k] > a[k];
     odd = odd || (valid && ((nonempty[k] && oe[k] == o[k]) || oe[k] < o[k] || b[k] < a[k]));
   }
-  if (__ballot(odd)) {
-#pragma unroll
-    for (int k = 0; k < K; k++)
-      if (nonempty[k] && oe[k] != o[k]) encode_literal_coop_global(in + a[k], b[k] - a[k], out + o[k], sm.code);
-    return;
-  }
-  if (ae <= A) return;  // no bytes (every literal empty)
-  const uint8_t *ia = in + A;
-  const uint8_t *ibase = ia - ((uintptr_t)ia & 15u);
-  uint8_t *oa = out + OA;
-  uint8_t *obase = oa - ((uintptr_t)oa & 15u);
-  const uint32_t odelta = (uint32_t)((uintptr_t)oa & 15u);
-  const uint32_t out_hi = odelta + (uint32_t)(oend - OA);             // the region's end, bytes from obase
-  const uint32_t a_first = (uint32_t)((uintptr_t)ia & 15u);           // A from ibase
-  const uint32_t b_rel = (uint32_t)((in + ae) - ibase);               // the range's end from ibase
-  // per literal: its first byte from ibase (~0: empty, never a start) and the
-  // bit position of its first code; per group, the span of its first bytes
-  uint32_t a_rel[K], q_lit[K], g_lo[K], g_hi[K];
-#pragma unroll
-  for (int k = 0; k < K; k++) {
-    a_rel[k] = nonempty[k] ? (uint32_t)((in + a[k]) - ibase) : ~0u;
-    q_lit[k] = 8u * (uint32_t)((out + o[k]) - obase);
-    g_lo[k] = (uint32_t)((in + uniform64(a[k])) - ibase);
-    const uint64_t a63 = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)a[k], kWave - 1) |
-                         ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(a[k] >> 32), kWave - 1) << 32);
-    g_hi[k] = (uint32_t)((in + a63) - ibase);
-  }
-  const uint32_t nchunk = (b_rel + 15u) >> 4;
-  const uint32_t nround = (nchunk + kWave - 1) / kWave;
-  const u32x4 *src = (const u32x4 *)ibase;
-  uint32_t carry = 0x80000000u | (8u * odelta);  // (round 0 starts at A, a literal start)
-  uint32_t flushed = 0;  // ring chunks stored so far (16-B chunks from obase)
-
-  auto flush = [&](uint32_t c0, uint32_t c1) {
-    for (uint32_t c = c0 + lane; c < c1; c += kWave) {
-#if MHQ_ENC_DIRECT
-      // words 4c .. 4c+3: slots 4c .. 4c+3 (mod kRingW)
-      u32x4 *p = (u32x4 *)(ring + ((4u * c) & (kRingW - 1u)));
-      u32x4 h = *p;
-      if (((4u * c) & (kRingW - 1u)) == 0u) {
-        h.x |= ring[kRingW];
-        ring[kRingW] = 0u;
-      }
-      const u32x4 w = u32x4{~__builtin_bswap32(h.x), ~__builtin_bswap32(h.y), ~__builtin_bswap32(h.z),
-                            ~__builtin_bswap32(h.w)};
-#else
-      // words 4c .. 4c+3: slots 4c+2 .. 4c+5 (two 8-B halves)
-      uint2 *p0 = (uint2 *)(ring + ((4u * c + 2u) & (kRingW - 1u)));
-      uint2 *p1 = (uint2 *)(ring + ((4u * c + 4u) & (kRingW - 1u)));
-      const uint2 h0 = *p0, h1 = *p1;
-      const u32x4 w = u32x4{~__builtin_bswap32(h0.x), ~__builtin_bswap32(h0.y), ~__builtin_bswap32(h1.x),
-                            ~__builtin_bswap32(h1.y)};
-#endif
-      const uint32_t lo = 16u * c, hi = lo + 16u;
-      if (lo >= odelta && hi <= out_hi) {
-        *(u32x4 *)(obase + lo) = w;
-      } else {
-        const uint32_t ww[4] = {w.x, w.y, w.z, w.w};
-        for (uint32_t x = max(lo, odelta); x < min(hi, out_hi); x++)
-          obase[x] = (uint8_t)(ww[(x - lo) >> 2] >> (8u * (x & 3u)));
-      }
-#if MHQ_ENC_DIRECT
-      *p = u32x4{0u, 0u, 0u, 0u};
-#else
-      *p0 = make_uint2(0u, 0u);
-      *p1 = make_uint2(0u, 0u);
-#endif
-    }
-  };
-
-  // loads run three rounds ahead (a wave's range is about three rounds on
-  // config 2: all of its input is requested at once)
-  u32x4 vb0 = u32x4{0u, 0u, 0u, 0u}, vb1 = vb0, vb2 = vb0;
-  if ((uint32_t)lane < nchunk) vb0 = __builtin_nontemporal_load(src + lane);  // aligned, holds a valid byte
-  if ((uint32_t)lane + kWave < nchunk) vb1 = __builtin_nontemporal_load(src + lane + kWave);
-  if ((uint32_t)lane + 2u * kWave < nchunk) vb2 = __builtin_nontemporal_load(src + lane + 2u * kWave);
-  for (uint32_t r = 0; r < nround; r++) {
-    const uint32_t lo = r * kRound;
-    // the round's literal starts: position and mask bit; the range's end acts
-    // as one more start, at the region's end (bytes after it land past the
-    // region and are never stored)
+  bool fallback = __ballot(odd) != 0;
+  if (!fallback && ae > A) {
+    const uint8_t *ia = in + A;
+    const uint8_t *ibase = ia - ((uintptr_t)ia & 15u);
+    uint8_t *oa = out + OA;
+    uint8_t *obase = oa - ((uintptr_t)oa & 15u);
+    const uint32_t odelta = (uint32_t)((uintptr_t)oa & 15u);
+    const uint32_t out_hi = odelta + (uint32_t)(oend - OA);  // the region's end, bytes from obase
+    const uint32_t b_rel = (uint32_t)((in + ae) - ibase);    // the range's end from ibase
+    // per literal: its first byte from ibase (~0: empty, never a start) and
+    // the bit position of its first code; per group, the span of its first bytes
+    uint32_t a_rel[K], q_lit[K], g_lo[K], g_hi[K];
 #pragma unroll
     for (int k = 0; k < K; k++) {
-      if (g_hi[k] >= lo && g_lo[k] < lo + kRound) {  // (wave-uniform: a group's starts lie in [g_lo, g_hi])
-        const uint32_t x = a_rel[k] - lo;
-        if (x < kRound) {
-          qtab[prow(x)] = q_lit[k];
-          atomicOr(&smask[x >> 5], 1u << (x & 31u));
+      a_rel[k] = nonempty[k] ? (uint32_t)((in + a[k]) - ibase) : ~0u;
+      q_lit[k] = kPB + 8u * (uint32_t)((out + o[k]) - obase);
+      g_lo[k] = (uint32_t)((in + uniform64(a[k])) - ibase);
+      const uint64_t a63 = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)a[k], kWave - 1) |
+                           ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(a[k] >> 32), kWave - 1) << 32);
+      g_hi[k] = (uint32_t)((in + a63) - ibase);
+    }
+    const uint32_t nchunk = (b_rel + 15u) >> 4;
+    const uint32_t nround = (nchunk + kWave - 1) / kWave;
+    ETL(2);
+    const u32x4 *src = (const u32x4 *)ibase;
+    // chunk c of the ring = bytes [16 c - 64, 16 c - 48) from obase; chunks
+    // 0-3 only ever hold the bytes before the first literal
+    const uint32_t end_chunk = (out_hi + 64u + 15u) >> 4;
+    // round 0, lane 0 starts 480 bits before the first literal (its <= 15
+    // bytes before A take <= 450 bits)
+    uint32_t carry = 0x80000000u | (kPB - 480u + 8u * odelta);
+    uint32_t flushed = 4;  // ring chunks stored (or never to be stored) so far
+
+    // Stores ring chunks [c0, c1) inverted: whole chunks inside the region as
+    // 16-B stores, the bytes of a chunk at either end that lie inside
+    // [odelta, out_hi) one by one; each chunk is then zeroed.
+    auto flush = [&](uint32_t c0, uint32_t c1) {
+      for (uint32_t c = c0 + lane; c < c1; c += kWave) {
+        u32x4 *p = (u32x4 *)(ring + ((4u * c) & (kRingW - 1u)));  // words 4c .. 4c+3
+        const u32x4 h = *p;
+        const u32x4 w = u32x4{~__builtin_bswap32(h.x), ~__builtin_bswap32(h.y), ~__builtin_bswap32(h.z),
+                              ~__builtin_bswap32(h.w)};
+        const uint32_t lo = 16u * c - 64u, hi = lo + 16u;
+        if (lo >= odelta && hi <= out_hi) {
+          *(u32x4 *)(obase + lo) = w;
+        } else {
+          const uint32_t ww[4] = {w.x, w.y, w.z, w.w};
+          for (uint32_t x = max(lo, odelta); x < min(hi, out_hi); x++)
+            obase[x] = (uint8_t)(ww[(x - lo) >> 2] >> (8u * (x & 3u)));
+        }
+        *p = u32x4{0u, 0u, 0u, 0u};
+      }
+    };
+
+    // loads run three rounds ahead; chunk indices are clamped to the last
+    // chunk (every lane loads: no predicated register copies; an aligned
+    // chunk holding a valid byte never crosses a page)
+    u32x4 vb0 = __builtin_nontemporal_load(src + min((uint32_t)lane, nchunk - 1u));
+    u32x4 vb1 = __builtin_nontemporal_load(src + min((uint32_t)lane + kWave, nchunk - 1u));
+    u32x4 vb2 = __builtin_nontemporal_load(src + min((uint32_t)lane + 2u * kWave, nchunk - 1u));
+    ETL(3);
+    // One round: consumes vb (loaded three rounds earlier) and reloads it for
+    // three rounds later.  The round loop is unrolled by three so that each
+    // buffer keeps its registers: a rotation (vb0 = vb1, ...) moves registers
+    // whose loads are still in flight, and the compiler waits for every
+    // outstanding load and store before such a move.  Returns false when the
+    // round's output would overflow the ring.
+    auto round = [&](const uint32_t r, u32x4 &vb) -> bool {
+      const uint32_t lo = r * kRound;
+      // the round's literal starts; the range's end acts as one more start,
+      // at the region's end
+#pragma unroll
+      for (int k = 0; k < K; k++) {
+        if (g_hi[k] >= lo && g_lo[k] < lo + kRound) {  // (wave-uniform: a group's starts lie in [g_lo, g_hi])
+          const uint32_t x = a_rel[k] - lo;
+          if (x < kRound) qtab[prow(x)] = q_lit[k];
         }
       }
-    }
-    if (lane == 0 && b_rel - lo < kRound) {
-      qtab[prow(b_rel - lo)] = 8u * out_hi;
-      atomicOr(&smask[(b_rel - lo) >> 5], 1u << ((b_rel - lo) & 31u));
-    }
-    const u32x4 v = vb0;
-    const uint32_t c = lo / 16u + lane;  // this lane's chunk
-    vb0 = vb1;
-    vb1 = vb2;
-    if (c + 3u * kWave < nchunk) vb2 = __builtin_nontemporal_load(src + c + 3u * kWave);
-    wave_sync();
-    const uint32_t mask = (smask[lane >> 1] >> (16u * (lane & 1u))) & 0xffffu;
-    uint32_t q16[16];
-    if (mask) {
+      if (lane == 0 && b_rel - lo < kRound) qtab[prow(b_rel - lo)] = kPB + 8u * out_hi;
+      const uint32_t c = lo / 16u + lane;  // this lane's chunk
+      const u32x4 v = c < nchunk ? vb : u32x4{kZeroBytes, kZeroBytes, kZeroBytes, kZeroBytes};
+      vb = __builtin_nontemporal_load(src + min(c + 3u * kWave, nchunk - 1u));
+      wave_sync();
+      uint32_t q16[16];
 #pragma unroll
       for (int j = 0; j < 4; j++) {
-        const u32x4 t = *(const u32x4 *)(qtab + prow(16u * lane + 4u * j));
+        u32x4 *qp = (u32x4 *)(qtab + prow(16u * lane + 4u * j));
+#if MHQ_ENC_X & 4
+        const u32x4 t = lane == 0 && j == 0 ? *qp : u32x4{0u, 0u, 0u, 0u};
+#else
+        const u32x4 t = *qp;
+        *qp = u32x4{0u, 0u, 0u, 0u};  // (read back before the zeroing: same lane, LDS in order)
+#endif
         q16[4 * j] = t.x;
         q16[4 * j + 1] = t.y;
         q16[4 * j + 2] = t.z;
         q16[4 * j + 3] = t.w;
       }
-    }
-    // code table lookups (complemented code, length)
-    uint32_t cd[16], ln[16];
-    {
-      const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+      // code table lookups (complemented left-aligned code, length)
+      uint32_t cd[16], ln[16];
+      {
+        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-      for (int k = 0; k < 16; k++) {
-        const uint2 t = sm.code[(w[k >> 2] >> (8 * (k & 3))) & 0xffu];
-        cd[k] = t.x;
-        ln[k] = t.y;
-      }
-    }
-    // bytes that belong to no literal of the wave: before A (round 0, lane 0)
-    // and in chunks past the range (the last round); wave-uniform branches,
-    // once per wave each (bytes after the range's end in its last chunk
-    // follow the end marker instead, past the region)
-    if (r == 0) {
-      const uint32_t below = lane == 0 ? a_first : 0u;
-#pragma unroll
-      for (int k = 0; k < 16; k++) {
-        cd[k] = (uint32_t)k < below ? 0u : cd[k];
-        ln[k] = (uint32_t)k < below ? 0u : ln[k];
-      }
-    }
-    if (r + 1 == nround) {
-      const bool past = c >= nchunk;
-#pragma unroll
-      for (int k = 0; k < 16; k++) {
-        cd[k] = past ? 0u : cd[k];
-        ln[k] = past ? 0u : ln[k];
-      }
-    }
-    // pass 1: the chunk's summary for the segmented scan
-    uint32_t acc = 0;
-#pragma unroll
-    for (int k = 0; k < 16; k++) {
-      acc = (mask >> k) & 1u ? q16[k] : acc;
-      acc += ln[k];
-    }
-    const uint32_t summ = (acc & 0x7fffffffu) | (mask ? 0x80000000u : 0u);
-    const uint32_t incl = seg_incl_scan(summ);
-    uint32_t excl = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)incl, 0x138, 0xf, 0xf, false);  // wave_shr:1
-    excl = lane == 0 ? 0u : excl;
-    // the position of the chunk's first byte: the carry, then lanes 0..l-1
-    const uint32_t start = ((int32_t)excl < 0 ? excl : carry + excl) & 0x7fffffffu;
-    const uint32_t last = __builtin_amdgcn_readlane((int32_t)incl, kWave - 1);
-    carry = ((int32_t)last < 0 ? last : carry + last) | 0x80000000u;
-#if MHQ_ENC_DIRECT
-    // pass 2: every code ORed into the ring where it lands: the word of its
-    // first bit takes L >> (pos % 32), the next word the rest (zero when the
-    // code fits); the left-aligned code L needs no length here
-    {
-      uint32_t pos = start;
-#pragma unroll
-      for (int k = 0; k < 16; k++) {
-        pos = (mask >> k) & 1u ? q16[k] : pos;  // a literal starts here
-        uint32_t *p = ring + __builtin_amdgcn_ubfe(pos, 5, 10);
-        atomicOr(p, __builtin_amdgcn_alignbit(0u, cd[k], pos));
-        atomicOr(p + 1, __builtin_amdgcn_alignbit(cd[k], 0u, pos));
-        pos += ln[k];
-      }
-    }
+        for (int k = 0; k < 16; k++) {
+#if MHQ_ENC_X & 1
+          cd[k] = w[k >> 2] << (8 * (k & 3));
+          ln[k] = 8u;
 #else
-    // pass 2: place the codes.  a64 holds bits [W - 64, W) of the output, MSB
-    // first; ring word j (bit 32 j) lives in slot (j + 2) % kRingW, so a
-    // window's top word is at byte address bfe(W, 3, 12).  A code ending past
-    // W first pushes the top word out (a code starting past W -- a gap before
-    // a literal -- restarts the window there).
-    uint32_t W = (start & ~31u) + 64u;
-    uint32_t pos = start;
-    uint64_t a64 = 0;
-#pragma unroll
-    for (int k = 0; k < 16; k++) {
-      pos = (mask >> k) & 1u ? q16[k] : pos;  // a literal starts here
-      const uint32_t end = pos + ln[k];
-      // the top word is complete once a code ends past the window: out it
-      // goes (twice at most on an exact layout: padding before a long code;
-      // a gap between literals -- a region longer than its code -- emits
-      // empty words until the code fits)
-#if MHQ_ENC_EMIT1
-      if (end > W) {  // one word out; a second only after a gap (rare: a branch of its own)
-        atomicOr((uint32_t *)((uint8_t *)ring + __builtin_amdgcn_ubfe(W, 3, 12)), (uint32_t)(a64 >> 32));
-        a64 <<= 32;
-        W += 32u;
-        while (end > W) {
-          atomicOr((uint32_t *)((uint8_t *)ring + __builtin_amdgcn_ubfe(W, 3, 12)), (uint32_t)(a64 >> 32));
-          a64 <<= 32;
-          W += 32u;
+          const uint2 t = sm.code[(w[k >> 2] >> (8 * (k & 3))) & 0xffu];
+          cd[k] = t.x;
+          ln[k] = t.y;
+#endif
         }
       }
-#else
-      while (end > W) {
-        atomicOr((uint32_t *)((uint8_t *)ring + __builtin_amdgcn_ubfe(W, 3, 12)), (uint32_t)(a64 >> 32));
-        a64 <<= 32;
-        W += 32u;
+      // pass 1: the chunk's summary for the segmented scan
+      uint32_t acc = 0;
+      bool any = false;
+#pragma unroll
+      for (int k = 0; k < 16; k++) {
+        acc = q16[k] != 0u ? q16[k] : acc;
+        any = any || q16[k] != 0u;
+        acc += ln[k];
       }
-#endif
-      a64 |= (uint64_t)cd[k] << (W - end);
-      pos = end;
+      const uint32_t summ = (acc & 0x7fffffffu) | (any ? 0x80000000u : 0u);
+      const uint32_t incl = seg_incl_scan(summ);
+      uint32_t excl = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)incl, 0x138, 0xf, 0xf, false);  // wave_shr:1
+      excl = lane == 0 ? 0u : excl;
+      // the position of the chunk's first byte: the carry, then lanes 0..l-1
+      const uint32_t start = ((int32_t)excl < 0 ? excl : carry + excl) & 0x7fffffffu;
+      const uint32_t last = __builtin_amdgcn_readlane((int32_t)incl, kWave - 1);
+      carry = ((int32_t)last < 0 ? last : carry + last) | 0x80000000u;
+      // the ring holds chunks [flushed, the carry's chunk]: one word short of
+      // the ring at most (a literal region much longer than its code)
+      if (((carry & 0x7fffffffu) >> 5) - 4u * flushed >= kRingW - 4u) return false;
+      // pass 2: the lane's codes in order through a two-word window (hi, lo)
+      // whose top word starts at bit wlo - 32; a code starting at pos lands
+      // in hi from bit pos % 32 on (alignbit shifts by pos % 32 only) and
+      // spills into lo.  Before a code that starts past the top word, that
+      // word is complete: it goes out (OR: the first and last words are
+      // shared with the neighbouring lanes) and the window moves on a word.
+      {
+        uint32_t pos = start, wlo = (start & ~31u) + 32u, hi = 0u, lw = 0u;
+#pragma unroll
+        for (int k = 0; k < 16; k++) {
+          pos = q16[k] != 0u ? q16[k] : pos;  // a literal starts here
+          if (pos >= wlo) {
+            if (!(MHQ_ENC_X & 2)) atomicOr(ring + (((wlo - 32u) >> 5) & (kRingW - 1u)), hi);
+            hi = lw;
+            lw = 0u;
+            wlo += 32u;
+            while (pos >= wlo) {  // a gap of a word or more (a region longer than its code)
+              atomicOr(ring + (((wlo - 32u) >> 5) & (kRingW - 1u)), hi);
+              hi = lw;
+              lw = 0u;
+              wlo += 32u;
+            }
+          }
+          hi |= __builtin_amdgcn_alignbit(0u, cd[k], pos);
+          lw |= __builtin_amdgcn_alignbit(cd[k], 0u, pos);
+          pos += ln[k];
+        }
+        if (MHQ_ENC_X & 2) {
+          if ((hi ^ lw) == 0x12345u) ring[lane] = hi;  // (keeps the values live)
+        } else {
+          if (hi) atomicOr(ring + (((wlo - 32u) >> 5) & (kRingW - 1u)), hi);
+          if (lw) atomicOr(ring + ((wlo >> 5) & (kRingW - 1u)), lw);
+        }
+      }
+      wave_sync();
+      if (r == 0 && lane < 4) ((u32x4 *)ring)[lane] = u32x4{0u, 0u, 0u, 0u};  // chunks 0-3: bytes before A
+      // every bit before the carry's position is final
+      const uint32_t done = min((carry & 0x7fffffffu) >> 7, end_chunk);
+      flush(flushed, done);
+      flushed = max(flushed, done);
+      wave_sync();
+      ETL(4 + (int)min(r, 58u));
+      return true;
+    };
+    for (uint32_t r = 0; r < nround && !fallback; r += 3) {
+      fallback = !round(r, vb0);
+      if (!fallback && r + 1 < nround) fallback = !round(r + 1, vb1);
+      if (!fallback && r + 2 < nround) fallback = !round(r + 2, vb2);
     }
-    if (a64 >> 32) atomicOr((uint32_t *)((uint8_t *)ring + __builtin_amdgcn_ubfe(W, 3, 12)), (uint32_t)(a64 >> 32));
-    if ((uint32_t)a64) atomicOr((uint32_t *)((uint8_t *)ring + __builtin_amdgcn_ubfe(W + 32u, 3, 12)), (uint32_t)a64);
-#endif
-    wave_sync();
-    if (lane < kRound / 32 + 2) smask[lane] = 0;  // (read above, before the wave_sync)
-    // every bit before the carry's position is final
-    const uint32_t done = min((carry & 0x7fffffffu) >> 7, (out_hi + 15u) >> 4);
-    flush(flushed, done);
-    flushed = max(flushed, done);
-    wave_sync();
+    if (!fallback) flush(flushed, end_chunk);
   }
-  flush(flushed, (out_hi + 15u) >> 4);
+  if (fallback) {  // (offsets read again: nothing of the above stays live through the rounds)
+    for (int k = 0; k < K; k++) {
+      const uint64_t i = s + (uint64_t)(kWave * k) + lane;
+      if (i < n) {
+        const uint64_t fa = in_off[i] - in_bias, fb = in_off[i + 1] - in_bias;
+        const uint64_t fo = out_off[i] - out_bias, foe = out_off[i + 1] - out_bias;
+        if (fb > fa && foe != fo) encode_literal_coop_global(in + fa, fb - fa, out + fo, sm.code);
+      }
+    }
+  }
+  ETL(63);
 }
 
 }  // namespace
+
+#ifdef MHQ_DIAG_ETL
+extern "C" int mhq_diag_etimeline(unsigned long long *out, int n) {
+  const int m = n < kEtlWaves * kEtlSlots ? n : kEtlWaves * kEtlSlots;
+  hipDeviceSynchronize();
+  const int rc = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_etl), m * sizeof(unsigned long long)) == hipSuccess ? kEtlSlots : -1;
+  static unsigned long long zeros[kEtlWaves * kEtlSlots];
+  hipMemcpyToSymbol(HIP_SYMBOL(g_etl), zeros, sizeof(zeros));
+  return rc;
+}
+#endif
 
 hipError_t launch_encode_len(const DevTables &t, const uint8_t *in, const uint64_t *in_off, uint64_t in_bias,
                              uint64_t n, uint32_t *enc_len, hipStream_t s, uint64_t *block_sums) {

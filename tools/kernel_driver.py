@@ -112,6 +112,43 @@ def timeline_report(fn):
         prev = np.where(a[:, b + 4] > 0, a[:, b + 4], prev)
 
 
+def etimeline_report(fn):
+    """Summarises the MHQ_DIAG_ETL build's per-wave coop-encode stamps (last
+    launch): [0] start, [1] table ready, [2] offsets used, [3] first loads
+    issued, [4 + r] round r done, [63] end."""
+    import ctypes
+
+    W, S = 16384, 64
+    buf = (ctypes.c_ulonglong * (W * S))()
+    fn(buf, W * S)
+    a = np.frombuffer(buf, dtype=np.uint64).reshape(W, S).astype(np.int64)
+    a = a[(a[:, 0] > 0) & (a[:, 63] > 0)]
+    t0 = a[:, 0].min()
+    us = lambda x: (x - t0) / 100.0  # noqa: E731
+    st = us(a[:, 0])
+    print(f"etl: {a.shape[0]} waves; start p10 {np.percentile(st, 10):.2f} p50 {np.percentile(st, 50):.2f} "
+          f"p90 {np.percentile(st, 90):.2f} max {st.max():.2f}; end p50 {np.percentile(us(a[:, 63]), 50):.2f} "
+          f"max {us(a[:, 63]).max():.2f} us", file=sys.stderr)
+    d = lambda k0, k1: (a[:, k1] - a[:, k0]) / 100.0  # noqa: E731
+    print(f"  per wave (mean us): table {d(0, 1).mean():.2f} offsets {d(1, 2).mean():.2f} issue {d(2, 3).mean():.2f} "
+          f"round0 {d(3, 4).mean():.2f} life {d(0, 63).mean():.2f}", file=sys.stderr)
+    nr = (a[:, 4:62] > 0).sum(axis=1)
+    rounds = []
+    for r in range(1, 12):
+        ok = nr > r
+        if ok.sum() < 10:
+            break
+        rounds.append(f"r{r} {((a[ok, 4 + r] - a[ok, 3 + r]) / 100.0).mean():.2f}")
+    last = a[np.arange(a.shape[0]), 3 + nr]
+    print(f"  rounds per wave mean {nr.mean():.2f}; round durations: " + " ".join(rounds) +
+          f"; tail (last round -> end) {((a[:, 63] - last) / 100.0).mean():.2f}", file=sys.stderr)
+    # by start generation
+    gen = np.digitize(st, np.percentile(st, [25, 50, 75]))
+    print("  by start quartile: " + " | ".join(
+        f"q{g}: start {st[gen == g].mean():.1f} life {d(0, 63)[gen == g].mean():.2f} "
+        f"round0 {d(3, 4)[gen == g].mean():.2f}" for g in range(4) if (gen == g).any()), file=sys.stderr)
+
+
 def wg_report(fn):
     """Summarises the MHQ_DIAG_WG build's stamps (last launch): stager tile
     timeline and decoder wait/work split, in us from the workgroup's start."""
@@ -243,6 +280,9 @@ def main():
     wg = getattr(_lib.load(), "mhq_diag_wg", None)
     if wg:
         wg_report(wg)
+    etl = getattr(_lib.load(), "mhq_diag_etimeline", None)
+    if etl:
+        etimeline_report(etl)
     tl = getattr(_lib.load(), "mhq_diag_timeline", None)
     if tl:
         timeline_report(tl)
