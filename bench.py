@@ -466,13 +466,14 @@ def config5(codec, dev, launches, rotate_bytes):
     return res
 
 
-def decode_only(codec, dev, steps, warmup, rotate_bytes):
-    """North-star decode-only rate: 2^20 x U{8..56} hdr literals."""
+def decode_only(codec, dev, steps, warmup, rotate_bytes, b=None):
+    """Decode-only rate of one 2^20-literal batch: by default the north star's
+    2^20 x U{8..56} hdr literals."""
     import torch
 
     from minhq_amd import workloads
 
-    b = workloads.north_star()
+    b = b if b is not None else workloads.north_star()
     data = torch.from_numpy(b.data).to(dev)
     off = torch.from_numpy(b.off.view(np.int64)).to(dev)
     dv = Dev(codec, data, off, dev)
@@ -680,6 +681,13 @@ def main():
     if rank == 0 and world == 1 and not args.no_extras:
         res["decode_only_northstar"] = decode_only(codec, dev, max(args.steps, 50), args.warmup,
                                                    args.rotate_gib * GIB)
+        # the other 2^20 shapes SURVEY.md §8(d) names: config 2 with printable
+        # bytes (codes up to 15 bits) and config 3 (the QIF corpus literals)
+        res["decode_only_shapes"] = {
+            "config2_print": decode_only(codec, dev, max(args.steps, 50), args.warmup, args.rotate_gib * GIB,
+                                         workloads.config2(1 << 20, "print")),
+            "config3_qif": decode_only(codec, dev, max(args.steps, 50), args.warmup, args.rotate_gib * GIB,
+                                       workloads.config3(1 << 20))}
         if not args.no_configs:
             res["config5"] = config5(codec, dev, max(args.steps, 10), args.rotate_gib * GIB)
     if rank == 0 and world == 1 and not args.no_cpu:

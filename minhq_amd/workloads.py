@@ -145,6 +145,33 @@ def config5(n: int = 4 << 20) -> Batch:
     return make_batch(n, "fixed", "adv", SEED_ADV, 128, 128, f"config5-{count_label(n)}x128B adv")
 
 
+def config3(n: int = 1 << 20) -> Batch:
+    """BASELINE.json configs[2]: the string literals of the reference's QIF
+    header sets -- the netbsd.qif fields (names and values) and the literals
+    embedded in hc/testcases_test.go / hc/qpack_test.go, as extracted into
+    tests/golden/ -- tiled to n literals."""
+    import json
+    import os
+
+    g = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests", "golden")
+    with open(os.path.join(g, "netbsd_qif.json")) as f:
+        fields = json.load(f)["fields"]
+    with open(os.path.join(g, "embedded_literals.json")) as f:
+        embedded = json.load(f)
+    lits = []
+    for fl in fields:
+        if fl:
+            lits += [fl[0].encode(), fl[1].encode()]
+    lits += [r["text"].encode() for r in embedded]
+    reps = n // len(lits) + 1
+    tiled = (lits * reps)[:n]
+    L = np.fromiter((len(x) for x in tiled), dtype=np.uint64, count=n)
+    off = np.zeros(n + 1, dtype=np.uint64)
+    off[1:] = np.cumsum(L, dtype=np.uint64)
+    data = np.frombuffer(b"".join(tiled), dtype=np.uint8).copy()
+    return Batch(data, off, f"config3-{count_label(n)}x qif corpus tiled")
+
+
 # ---- the same batches generated on a device (torch) ------------------------
 # Bit-identical to make_batch: splitmix64 in wrapping int64 arithmetic
 # (logical shifts by masking), the same float64 unit values and CDFs.  Used for

@@ -29,21 +29,8 @@ def batch_for(name: str, n: int):
         return w.config2(n or (1 << 20))
     if name == "config2print":
         return w.config2(n or (1 << 20), "print")
-    if name == "config3":  # the QIF corpus substitute: netbsd.qif's literals (+ test texts) tiled to 2^20
-        import json
-        import os
-
-        from minhq_amd import hc
-        g = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests", "golden")
-        lits = []
-        for f in json.load(open(os.path.join(g, "netbsd_qif.json")))["fields"]:
-            if f:
-                lits += [f[0].encode(), f[1].encode()]
-        lits += [r["text"].encode() for r in json.load(open(os.path.join(g, "embedded_literals.json")))]
-        total = n or (1 << 20)
-        tiled = (lits * (total // len(lits) + 1))[:total]
-        data, off = hc.pack(tiled)
-        return w.Batch(data, off, "config3-qif corpus tiled 1M")
+    if name == "config3":  # the QIF corpus: netbsd.qif's literals (+ test texts) tiled to 2^20
+        return w.config3(n or (1 << 20))
     if name == "config4":
         return w.config4(n or (1 << 22))
     if name == "config5":
