@@ -22,6 +22,7 @@ os.makedirs(dst, exist_ok=True)
 
 KERNELS = {"decode_kernel": "decode_kernel", "encode_kernel<true>": "encode_kernel",
            "encode_kernel<false>": "encode_len_kernel", "encode_len_kernel": "encode_len_kernel",
+           "encode_coop_kernel": "encode_coop_kernel",
            "scan_apply_kernel": "scan_apply_kernel",
            "scan_reduce_kernel": "scan_reduce_kernel", "scan_kernel": "scan_kernel"}
 
