@@ -24,6 +24,7 @@
 //     thread straight from global memory.
 #include <hip/hip_runtime.h>
 #include <stdlib.h>
+#include <string.h>
 
 #include <algorithm>
 
@@ -52,6 +53,9 @@
 #ifndef MHQ_ENC_SHORT_MEAN  // mean plaintext bytes up to which a workgroup takes one range of kT literals
 #define MHQ_ENC_SHORT_MEAN 40
 #endif
+#ifndef MHQ_ENC_TINY_MEAN  // mean plaintext bytes up to which the cooperative kernel encodes (per-literal costs)
+#define MHQ_ENC_TINY_MEAN 20
+#endif
 
 namespace mhq {
 namespace {
@@ -64,6 +68,14 @@ constexpr int kOutCap = MHQ_ENC_OUTCAP;
 constexpr int kPF = (kInCap / 16 + kT - 1) / kT;  // prefetched input chunks per thread
 constexpr int kBuckets = 64;
 constexpr uint32_t kShortMean = MHQ_ENC_SHORT_MEAN;
+constexpr uint32_t kTinyMean = MHQ_ENC_TINY_MEAN;
+// The thread-per-literal kernel's batches: a mean literal over kTinyMean and
+// up to kShortMean bytes (config 2 and the north star); the cooperative
+// kernel takes the rest (shorter: config 3's QIF literals, 26.6 us against
+// 38.3; longer: configs 4 and 5).
+__device__ __forceinline__ bool thread_form(uint64_t bytes, uint64_t n) {
+  return bytes > (uint64_t)kTinyMean * n && bytes <= (uint64_t)kShortMean * n;
+}
 
 template <bool kEmit>
 struct Smem {
@@ -238,11 +250,14 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu((kT / 64 * M
     const uint8_t *__restrict__ in, const uint64_t *__restrict__ in_off, uint64_t in_bias, uint64_t n,
     uint8_t *__restrict__ out, const uint64_t *__restrict__ out_off, uint64_t out_bias,
     uint32_t *__restrict__ enc_len, const uint32_t *__restrict__ g_code, const uint8_t *__restrict__ g_len,
-    uint64_t per_block, uint32_t n_persist) {
+    uint64_t per_block, uint32_t n_persist, uint32_t long_elsewhere) {
   __shared__ Smem<kEmit> sm;
   const uint32_t tid = threadIdx.x;
   const uint32_t lane = tid % kWave;
   const uint32_t wave = tid / kWave;
+  // long_elsewhere: a batch outside the thread form's band (thread_form) is
+  // the cooperative kernel's, launched beside this one: end at once
+  if (long_elsewhere && !thread_form(in_off[n] - in_off[0], n)) return;
   // Two grids in one launch (the grid holds max(ceil(n / kT), n_persist)
   // workgroups): short literals (a mean under kShortMean bytes, so kT of them
   // fill about one staging slice) take one range of kT literals per
@@ -715,9 +730,13 @@ __global__ __launch_bounds__(kCT) void encode_coop_kernel(const uint8_t *__restr
                                                           uint64_t n, uint8_t *__restrict__ out,
                                                           const uint64_t *__restrict__ out_off, uint64_t out_bias,
                                                           const uint32_t *__restrict__ g_code,
-                                                          const uint8_t *__restrict__ g_len) {
+                                                          const uint8_t *__restrict__ g_len,
+                                                          uint32_t short_elsewhere) {
   __shared__ CoopSmem sm;
   const uint32_t tid = threadIdx.x, lane = tid % kWave, wave = tid / kWave;
+  // short_elsewhere: a batch in the thread form's band (thread_form) is
+  // encode_kernel's, launched beside this one: end at once
+  if (short_elsewhere && thread_form(in_off[n] - in_off[0], n)) return;
   ETL(0);
   // the wave's literals: K groups of 64, [s, s + 64 K); their offsets are
   // requested first so that the loads overlap the table set-up
@@ -985,14 +1004,37 @@ hipError_t launch_encode_len(const DevTables &t, const uint8_t *in, const uint64
 hipError_t launch_encode(const DevTables &t, const uint8_t *in, const uint64_t *in_off, uint64_t in_bias,
                          uint64_t n, uint8_t *out, const uint64_t *out_off, uint64_t out_bias, hipStream_t s) {
   if (n == 0) return hipSuccess;
-#if MHQ_ENC_COOP
-  // K groups of 64 literals per wave: as many as keep about two waves per
-  // SIMD slot (16 per CU) busy
-  // (MHQ_ENC_K in the environment fixes K: tests and tuning)
+  // Two forms, picked on the device by the batch's mean literal (the host
+  // does not know the byte count of a device batch, thread_form): from
+  // kTinyMean to kShortMean bytes the thread-per-literal kernel (config 2:
+  // 37 us against 47.6 for the cooperative one), outside that band the
+  // wave-cooperative kernel (config 3 1.4x, config 4 1.4x, config 5 2.5x
+  // faster).  Both are launched; the one the mean does not pick reads the
+  // batch's two bounds and ends.  MHQ_ENC_FORM=thread|coop in the
+  // environment forces a form, as MHQ_ENC_K (K groups per coop wave) forces
+  // the cooperative one: tests and tuning.
   static const int k_env = [] {
     const char *e = getenv("MHQ_ENC_K");
     return e ? atoi(e) : 0;
   }();
+  static const int form = [] {  // 0 by the mean, 1 thread, 2 coop
+    const char *e = getenv("MHQ_ENC_FORM");
+    if (e && !strcmp(e, "thread")) return 1;
+    if ((e && !strcmp(e, "coop")) || k_env) return 2;
+    return MHQ_ENC_COOP ? 0 : 1;
+  }();
+  if (form != 2) {
+    // persistent form: MHQ_ENC_BLOCKS resident workgroups per CU (never more than the tiles)
+    const unsigned persist = dev::tile_grid((n + kT - 1) / kT, 1, MHQ_ENC_BLOCKS * MHQ_PER_CU);
+    const uint64_t tiles = (n + kT - 1) / kT;
+    const unsigned grid = (unsigned)(tiles > persist ? tiles : persist);
+    encode_kernel<true><<<dim3(grid), dim3(kT), 0, s>>>(in, in_off, in_bias, n, out, out_off, out_bias, nullptr,
+                                                         t.code, t.len, (n + persist - 1) / persist, persist,
+                                                         form == 0 ? 1u : 0u);
+    if (form == 1) return hipGetLastError();
+  }
+  // K groups of 64 literals per wave: as many as keep about two waves per
+  // SIMD slot (16 per CU) busy
   int K = MHQ_ENC_K ? MHQ_ENC_K : k_env;
   if (K == 0) {
     const uint64_t slots = (uint64_t)dev::device_cus() * 16u * 2u;
@@ -1001,20 +1043,13 @@ hipError_t launch_encode(const DevTables &t, const uint8_t *in, const uint64_t *
   }
   const uint64_t per_wg = (uint64_t)kCT * K;
   const dim3 cgrid((unsigned)((n + per_wg - 1) / per_wg));
+  const uint32_t se = form == 0 ? 1u : 0u;
   switch (K) {
-    case 1: encode_coop_kernel<1><<<cgrid, dim3(kCT), 0, s>>>(in, in_off, in_bias, n, out, out_off, out_bias, t.code, t.len); break;
-    case 2: encode_coop_kernel<2><<<cgrid, dim3(kCT), 0, s>>>(in, in_off, in_bias, n, out, out_off, out_bias, t.code, t.len); break;
-    case 4: encode_coop_kernel<4><<<cgrid, dim3(kCT), 0, s>>>(in, in_off, in_bias, n, out, out_off, out_bias, t.code, t.len); break;
-    default: encode_coop_kernel<8><<<cgrid, dim3(kCT), 0, s>>>(in, in_off, in_bias, n, out, out_off, out_bias, t.code, t.len); break;
+    case 1: encode_coop_kernel<1><<<cgrid, dim3(kCT), 0, s>>>(in, in_off, in_bias, n, out, out_off, out_bias, t.code, t.len, se); break;
+    case 2: encode_coop_kernel<2><<<cgrid, dim3(kCT), 0, s>>>(in, in_off, in_bias, n, out, out_off, out_bias, t.code, t.len, se); break;
+    case 4: encode_coop_kernel<4><<<cgrid, dim3(kCT), 0, s>>>(in, in_off, in_bias, n, out, out_off, out_bias, t.code, t.len, se); break;
+    default: encode_coop_kernel<8><<<cgrid, dim3(kCT), 0, s>>>(in, in_off, in_bias, n, out, out_off, out_bias, t.code, t.len, se); break;
   }
-  return hipGetLastError();
-#endif
-  // persistent form: MHQ_ENC_BLOCKS resident workgroups per CU (never more than the tiles)
-  const unsigned persist = dev::tile_grid((n + kT - 1) / kT, 1, MHQ_ENC_BLOCKS * MHQ_PER_CU);
-  const uint64_t tiles = (n + kT - 1) / kT;
-  const unsigned grid = (unsigned)(tiles > persist ? tiles : persist);
-  encode_kernel<true><<<dim3(grid), dim3(kT), 0, s>>>(in, in_off, in_bias, n, out, out_off, out_bias, nullptr, t.code,
-                                                       t.len, (n + persist - 1) / persist, persist);
   return hipGetLastError();
 }
 

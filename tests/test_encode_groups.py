@@ -18,8 +18,9 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 CHILD = r'''
-import random, sys
+import os, random, sys
 import numpy as np, torch
+THREAD = os.environ.get("MHQ_ENC_FORM") == "thread"
 sys.path.insert(0, ".")
 from minhq_amd import hc
 from oracle import oracle
@@ -53,7 +54,10 @@ def run(lits, ibias=0, obias=0, slack=None, skip=None, seed=0):
             continue
         r = ref[int(exact[i]):int(exact[i + 1])]
         assert got[g0:g0 + len(r)].tobytes() == r.tobytes(), ("literal", i, n)
-        assert (got[g0 + len(r):g0 + int(reg[i])] == 0xFF).all(), ("slack", i)
+        # (bytes past enc_len are unspecified, mhq_huff.h; the cooperative
+        # kernel's complemented ring leaves them all ones)
+        if not THREAD:
+            assert (got[g0 + len(r):g0 + int(reg[i])] == 0xFF).all(), ("slack", i)
 
 rng = random.Random(99)
 run([bytes(rng.randrange(256) for _ in range(rng.randrange(0, 90))) for _ in range(5000)])
@@ -77,9 +81,11 @@ print("ok")
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("k", [1, 2, 4, 8])
+@pytest.mark.parametrize("k", [1, 2, 4, 8, "thread"])
 def test_encode_literal_groups(k):
-    env = dict(os.environ, MHQ_ENC_K=str(k))
+    # "thread": the thread-per-literal kernel for every batch (MHQ_ENC_FORM),
+    # which the launch otherwise picks only for batches of short literals
+    env = dict(os.environ, MHQ_ENC_FORM="thread") if k == "thread" else dict(os.environ, MHQ_ENC_K=str(k))
     r = subprocess.run([sys.executable, "-c", CHILD], env=env, cwd=ROOT, capture_output=True, text=True,
                        timeout=240)
     assert r.returncode == 0 and "ok" in r.stdout, r.stdout[-3000:] + r.stderr[-3000:]

@@ -8,6 +8,7 @@
 //   2  one 8-bit probe per symbol (T8, 16 bank-interleaved copies), four
 //      probes per step, LUT2 at the step's first probe only
 //   3  variant 0 with a third LUT1 probe per step
+//   4-11  variant 0 with one change (kMode below); 12 one output store per two steps
 // Prints G symbols/s chip-wide and cycles per step per wave for 8/12/16
 // waves per CU.  Every variant checks its bytes against the symbol stream.
 //
@@ -17,6 +18,7 @@
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
+#include <string.h>
 
 #include <vector>
 
@@ -228,7 +230,10 @@ __device__ uint32_t run(Smem &sm, uint32_t p0, uint32_t p1, uint32_t eb, uint32_
   if (V == 1) b.init(sm, p1, eb, (threadIdx.x & 1023u) * 60u + 30u * 1024u);
   bool stop;
   for (uint32_t i = 0; i < iters; i++) {
-    if (V >= 4) {
+    if (V == 12) {  // one output store per two steps (timing only: the first step stores nothing)
+      masked_step<false, false, 7>(sm, sm.out_w, a.in, a.out, a.pend, stop, glut, lane);
+      masked_step<true, false, 0>(sm, sm.out_w, a.in, a.out, a.pend, stop, glut, lane);
+    } else if (V >= 4) {
       masked_step<false, false, V>(sm, sm.out_w, a.in, a.out, a.pend, stop, glut, lane);
       masked_step<true, false, V>(sm, sm.out_w, a.in, a.out, a.pend, stop, glut, lane);
     } else if (V == 0 || V == 1 || V == 3) {
@@ -424,8 +429,22 @@ int main(int argc, char **argv) {
   CHECK(hipEventCreate(&e0));
   CHECK(hipEventCreate(&e1));
   const int wavess[] = {8, 12, 16};
-  for (int v = 0; v < 12; v++) {
-    if (v >= 1 && v <= 6) continue;
+  const char *only = argc > 2 ? argv[2] : nullptr;  // comma-separated variants to time (default: all but 2, 3)
+  for (int v = 0; v < 13; v++) {
+    if (only) {
+      char key[8];
+      snprintf(key, sizeof key, "%d", v);
+      bool hit = false;
+      for (const char *p = only; *p;) {
+        const char *q = strchr(p, ',');
+        const size_t len = q ? (size_t)(q - p) : strlen(p);
+        if (len == strlen(key) && !strncmp(p, key, len)) hit = true;
+        p += len + (q ? 1 : 0);
+      }
+      if (!hit) continue;
+    } else if (v >= 2 && v <= 3) {
+      continue;
+    }
     for (int waves : wavess) {
       auto launch = [&]() {
         dim3 grid(cus), block(waves * 64);
@@ -440,6 +459,7 @@ int main(int argc, char **argv) {
         if (v == 7) ubench<7><<<grid, block>>>(d_lut1, d_lut2, d_t8, d_words, d_starts, ns, iters, d_sink, d_bits, d_cyc);
         if (v == 9) ubench<9><<<grid, block>>>(d_lut1, d_lut2, d_t8, d_words, d_starts, ns, iters, d_sink, d_bits, d_cyc);
         if (v == 10) ubench<10><<<grid, block>>>(d_lut1, d_lut2, d_t8, d_words, d_starts, ns, iters, d_sink, d_bits, d_cyc);
+        if (v == 12) ubench<12><<<grid, block>>>(d_lut1, d_lut2, d_t8, d_words, d_starts, ns, iters, d_sink, d_bits, d_cyc);
         if (v == 11) ubench<11><<<grid, block>>>(d_lut1, d_lut2, d_t8, d_words, d_starts, ns, iters, d_sink, d_bits, d_cyc);
         if (v == 8) ubench<8><<<grid, block>>>(d_lut1, d_lut2, d_t8, d_words, d_starts, ns, iters, d_sink, d_bits, d_cyc);
       };
