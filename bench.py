@@ -220,14 +220,21 @@ def load_traffic(path, kernel):
         return None
 
 
-def _threads():
-    env = os.environ.get("OMP_NUM_THREADS")
-    if env and env.isdigit() and int(env) > 0:
-        return int(env)
+def _affinity():
     try:
         return len(os.sched_getaffinity(0))
     except Exception:
         return os.cpu_count() or 1
+
+
+def _threads():
+    """(threads, where the count comes from): OMP_NUM_THREADS when set -- the
+    GPU box sets it to 16, this process's share of a host whose affinity mask
+    spans every core -- else the CPU affinity of this process."""
+    env = os.environ.get("OMP_NUM_THREADS")
+    if env and env.isdigit() and int(env) > 0:
+        return int(env), "OMP_NUM_THREADS"
+    return _affinity(), "sched_getaffinity"
 
 
 def cpu_baseline(batch, seconds: float):
@@ -238,7 +245,7 @@ def cpu_baseline(batch, seconds: float):
     from oracle import oracle
 
     oracle.build()
-    cores = _threads()
+    cores, cores_src = _threads()
     m = min(batch.n, 1 << 17)
     off = batch.off[: m + 1].copy()
     data = batch.data[: int(off[-1])].copy()
@@ -274,6 +281,7 @@ def cpu_baseline(batch, seconds: float):
     f_one, _, _ = rate(lambda: oracle.decode_batch(enc, eoff, cap, 1, fast=True), leg / 2)
     d_all, _, _ = rate(lambda: oracle.decode_batch(enc, eoff, cap, cores), leg / 2)
     return {"value": round(v_all, 4), "unit": "GiB/s", "cores": cores, "kind": "port",
+            "cores_source": cores_src, "affinity_cpus": _affinity(), "os_cpu_count": os.cpu_count(),
             "sample": f"first {m} literals of the workload, encode+decode, {n_all} passes in {t_all:.1f}s on "
                       f"{cores} threads (minhq hc/huffman.go + io/bitio.go bit-serial algorithm restated in C, "
                       f"oracle/huff_oracle.c; os.cpu_count()={os.cpu_count()})",

@@ -87,7 +87,10 @@ constexpr int kWOut = MHQ_DEC_WOUT;     // output slice bytes (from the tile's 1
 constexpr int kBuckets = 64;
 static_assert(kWOut % 16 == 0, "output slice must be whole 16-B chunks");
 
-struct WaveSmem {
+#ifndef MHQ_DEC_ALIGN  // a wave slice's alignment (16: its 16-B LDS accesses are single ds_*_b128)
+#define MHQ_DEC_ALIGN 16
+#endif
+struct alignas(MHQ_DEC_ALIGN) WaveSmem {
   uint32_t in_w[kWIn / 4 + 4];    // stream words, byte-swapped; +4 words of look-ahead slack
   uint32_t out_w[kWOut / 4 + 4];  // output staging (global layout, zero-filled); +4 words slack
   uint32_t rec[kTile + 1];        // per boundary: input byte index | output byte index << 16

@@ -77,8 +77,11 @@ __device__ __forceinline__ bool thread_form(uint64_t bytes, uint64_t n) {
   return bytes > (uint64_t)kTinyMean * n && bytes <= (uint64_t)kShortMean * n;
 }
 
+#ifndef MHQ_ENC_ALIGN  // the thread kernel's LDS alignment (16: its 16-B LDS accesses are single ds_*_b128)
+#define MHQ_ENC_ALIGN 16
+#endif
 template <bool kEmit>
-struct Smem {
+struct alignas(MHQ_ENC_ALIGN) Smem {
   uint2 code[256];                // (code right-justified, length)
   uint32_t in_w[kInCap / 4 + 4];  // plaintext, natural byte order
   uint32_t out_w[kEmit ? kOutCap / 4 + 4 : 4];  // output staging (global layout, zero-filled)
@@ -662,7 +665,7 @@ constexpr uint32_t kRingW = 1024;  // output ring words per wave (4 KiB)
 constexpr uint32_t kPB = 512;      // bit positions start 64 bytes before the wave's output base
 constexpr uint32_t kZeroBytes = 0x30303030u;  // '0' x 4: 5-bit codes for chunks past the range
 
-struct CoopSmem {
+struct alignas(16) CoopSmem {
   uint2 code[256];                 // (complemented code, left-aligned; length)
   uint32_t ring[kCW][kRingW];      // complemented output words (MSB-first values), zero where unwritten
   uint32_t qtab[kCW][kRound];      // (prow) output bit position of a literal starting at a byte; 0: none
@@ -738,9 +741,22 @@ __global__ __launch_bounds__(kCT) void encode_coop_kernel(const uint8_t *__restr
   // encode_kernel's, launched beside this one: end at once
   if (short_elsewhere && thread_form(in_off[n] - in_off[0], n)) return;
   ETL(0);
-  // the wave's literals: K groups of 64, [s, s + 64 K); their offsets are
-  // requested first so that the loads overlap the table set-up
-  const uint64_t s = ((uint64_t)blockIdx.x * kCW + wave) * (uint64_t)(kWave * K);
+  // the code table; the waves are independent after the barrier
+  {
+    const uint32_t L = g_len[tid];
+    const uint32_t c = ~g_code[tid] & ((1u << L) - 1u);
+    sm.code[tid] = make_uint2(c << (32u - L), L);  // left-aligned (every length is 5..30)
+  }
+  uint32_t *ring = sm.ring[wave];
+  uint32_t *qtab = sm.qtab[wave];
+  __syncthreads();
+  ETL(1);
+  // Persistent: wave w takes the ranges of K groups of 64 literals
+  // [s, s + 64 K), s = 64 K (w + j * waves in the grid), j = 0, 1, ...: one
+  // generation of waves (the launch holds at most what stays resident), so a
+  // launch that ends at once (short_elsewhere) costs only that generation.
+  const uint64_t stride = (uint64_t)gridDim.x * kCW * (uint64_t)(kWave * K);
+  for (uint64_t s = ((uint64_t)blockIdx.x * kCW + wave) * (uint64_t)(kWave * K); s < n; s += stride) {
   uint64_t a[K], o[K];
 #pragma unroll
   for (int k = 0; k < K; k++) {
@@ -750,21 +766,12 @@ __global__ __launch_bounds__(kCT) void encode_coop_kernel(const uint8_t *__restr
   }
   const uint64_t ae = in_off[min(s + (uint64_t)(kWave * K), n) + vzero()] - in_bias;
   const uint64_t oend = out_off[min(s + (uint64_t)(kWave * K), n) + vzero()] - out_bias;
-  {
-    const uint32_t L = g_len[tid];
-    const uint32_t c = ~g_code[tid] & ((1u << L) - 1u);
-    sm.code[tid] = make_uint2(c << (32u - L), L);  // left-aligned (every length is 5..30)
-  }
-  uint32_t *ring = sm.ring[wave];
-  uint32_t *qtab = sm.qtab[wave];
 #pragma unroll
-  for (int k = 0; k < 4; k++) {
+  for (int k = 0; k < 4; k++) {  // (a range that fell back, or ended past its region, leaves words behind)
     ((u32x4 *)ring)[lane + kWave * k] = u32x4{0u, 0u, 0u, 0u};
     ((u32x4 *)qtab)[lane + kWave * k] = u32x4{0u, 0u, 0u, 0u};
   }
-  __syncthreads();  // the code table; the waves are independent from here on
-  ETL(1);
-  if (s >= n) return;
+  wave_sync();
   const uint64_t A = uniform64(a[0]), OA = uniform64(o[0]);
   // layouts the ring cannot express: a literal whose output region is empty
   // (the caller skips it, mhq_huff.h), offsets out of order, or a range over
@@ -977,6 +984,8 @@ __global__ __launch_bounds__(kCT) void encode_coop_kernel(const uint8_t *__restr
       }
     }
   }
+  wave_sync();
+  }
   ETL(63);
 }
 
@@ -1039,10 +1048,14 @@ hipError_t launch_encode(const DevTables &t, const uint8_t *in, const uint64_t *
   if (K == 0) {
     const uint64_t slots = (uint64_t)dev::device_cus() * 16u * 2u;
     K = 1;
-    while (K < 8 && (n + (uint64_t)kWave * 2 * K - 1) / ((uint64_t)kWave * 2 * K) >= slots) K *= 2;
+    while (K < 4 && (n + (uint64_t)kWave * 2 * K - 1) / ((uint64_t)kWave * 2 * K) >= slots) K *= 2;
+    // (K = 8 builds at 131 VGPRs, three waves per SIMD: the resident grid
+    // below assumes four; larger batches loop over more ranges instead)
   }
   const uint64_t per_wg = (uint64_t)kCT * K;
-  const dim3 cgrid((unsigned)((n + per_wg - 1) / per_wg));
+  // at most one resident generation: 4 workgroups of 34 KiB LDS per CU
+  const uint64_t resident = (uint64_t)dev::device_cus() * 4u;
+  const dim3 cgrid((unsigned)std::min<uint64_t>((n + per_wg - 1) / per_wg, resident));
   const uint32_t se = form == 0 ? 1u : 0u;
   switch (K) {
     case 1: encode_coop_kernel<1><<<cgrid, dim3(kCT), 0, s>>>(in, in_off, in_bias, n, out, out_off, out_bias, t.code, t.len, se); break;

@@ -7,7 +7,8 @@ against the oracle (oracle/huff_oracle.c, the restated hc/huffman.go:23-37
 Write + Pad) on batches that stress the round/mark logic: random bytes (long
 codes), tiny and empty literals (many starts per 16-B chunk), long literals
 beside short ones, unaligned input and output bases, output regions with
-slack, a partial last group, and empty regions (the fallback path).
+slack, a partial last group, empty regions (the fallback path), and a
+2^20-literal batch, more ranges than the persistent grid's resident waves.
 """
 import os
 import subprocess
@@ -76,6 +77,13 @@ run(tiny[:9000], slack=nr.integers(0, 4, 9000))
 skip = nr.random(9000) < 0.01
 run(tiny[:9000], skip=skip)
 run([bytes([255] * 4000), b"a", bytes(range(256)) * 7])
+# more ranges than the resident waves (1,024 workgroups x 4 waves): every
+# wave of the persistent grid loops over several ranges
+big = np.random.default_rng(7)
+lens = big.integers(0, 48, 1 << 20)
+blob = big.integers(32, 127, int(lens.sum()), dtype=np.uint8).tobytes()
+cuts = np.concatenate([[0], np.cumsum(lens)])
+run([blob[cuts[i]:cuts[i + 1]] for i in range(1 << 20)], ibias=7, obias=3)
 print("ok")
 '''
 
