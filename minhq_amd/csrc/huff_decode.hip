@@ -68,6 +68,12 @@
 #ifndef MHQ_DEC_SOPEN  // 1: the first tile's input loads are addressed by two scalar loads (no wait for the offsets)
 #define MHQ_DEC_SOPEN 0
 #endif
+#ifndef MHQ_DEC_OPTIMISTIC  // 1: literals whose region may truncate run the fast loop, checked after (see decode_piece)
+#define MHQ_DEC_OPTIMISTIC 1
+#endif
+#ifndef MHQ_DEC_ENDOR  // 1: a literal's last output word is OR-ed in the end branch (0: by the next step)
+#define MHQ_DEC_ENDOR 0
+#endif
 #ifndef MHQ_DEC_WOUT  // a wave's output slice (bytes, multiple of 16)
 #define MHQ_DEC_WOUT 6448
 #endif
@@ -429,6 +435,10 @@ struct LitRef {
   // The output region holds floor(bits/5) bytes, the most any input can
   // produce: no room check is needed.
   __device__ __forceinline__ bool roomy() const { return oend - optr >= (endbit - p) / 5u; }
+  // The most this literal can produce stays inside the output slice (its
+  // last word included): run past a short region, it can only spoil bytes
+  // that a redo of the piece re-zeroes, or the slice's unused tail.
+  __device__ __forceinline__ bool in_slice() const { return optr + (endbit - p) / 5u + 4u <= (uint32_t)kWOut + 16u; }
 };
 
 #ifdef MHQ_DIAG_COUNT
@@ -642,12 +652,16 @@ __device__ __forceinline__ void decode_piece(const Smem &sm, WaveSmem &ws, uint3
 #if MHQ_DEC_PRIO
   __builtin_amdgcn_s_setprio(0);  // the probe loop at normal priority
 #endif
-  // Every literal whose region cannot truncate runs the masked loop to its
-  // end (ones past the end: no end test, no separate tail loop); the lane
-  // moves from A to B in place.  A literal with a code across its end (not
-  // well formed) and one whose region truncates take the checked loop.
+  // Every literal runs the masked loop to its end (ones past the end: no end
+  // test, no separate tail loop); the lane moves from A to B in place.  A
+  // literal with a code across its end (not well formed) takes the checked
+  // loop.  So does, since round 3, a piece in which a literal whose region
+  // can truncate (under floor(8 bits / 5) bytes) turned out not to fit it
+  // (below): regions sized to the exact plaintext -- a caller that knows the
+  // lengths, as every round trip does -- stay on the fast loop.
   constexpr uint32_t kRedo = 0xffffffffu;
-  const bool roomA = hasA && A.roomy(), roomB = hasB && B.roomy();
+  const bool roomA = hasA && (A.roomy() || (MHQ_DEC_OPTIMISTIC && A.in_slice()));
+  const bool roomB = hasB && (B.roomy() || (MHQ_DEC_OPTIMISTIC && B.in_slice()));
   uint32_t rA = kRedo, rB = kRedo;
   {
     BitBufM in, inB;  // inB: B's stream, set up once for the in-loop switch
@@ -678,8 +692,13 @@ __device__ __forceinline__ void decode_piece(const Smem &sm, WaveSmem &ws, uint3
       if (masked_step(sm, ws.out_w, in, out, pend, stop)) {
         // stop: the EOS prefix at p (INVALID when a 31st bit of the literal follows)
         const uint32_t r = in.left < 0 ? kRedo : (out.optr() - ost) | ((uint32_t)(in.left > kEosOnes) << 31);
+#if MHQ_DEC_ENDOR
         atomicOr(&ws.out_w[pend.ow], pend.v);  // the literal's last word
         pend.v = 0u;
+#endif
+        // (otherwise the literal's last word stays in `pend`: the next step
+        // ORs it before anything else, as every step does its predecessor's,
+        // and the loop's end ORs the last one -- no extra LDS store here)
         rA = onB ? rA : r;
         rB = onB ? r : rB;
         active = !onB && roomB;
@@ -689,7 +708,34 @@ __device__ __forceinline__ void decode_piece(const Smem &sm, WaveSmem &ws, uint3
         onB = true;
       }
     }
+#if !MHQ_DEC_ENDOR
+    atomicOr(&ws.out_w[pend.ow], pend.v);
+#endif
   }
+#if MHQ_DEC_OPTIMISTIC
+  {
+    // A fast result for a region that can truncate stands when it fits: a
+    // longer output has run past the region into a neighbour's bytes, and an
+    // INVALID literal that fills its region exactly is OK to the reference
+    // (Read returns once its buffer is full, hc/huffman.go:104, before the
+    // bits after).  Otherwise the whole piece is decoded again by the checked
+    // loop over a re-zeroed output region.
+    auto overflow = [](const LitRef<kGaps> &L, uint32_t r) {
+      const uint32_t len = r & 0x7fffffffu, region = L.oend - L.optr;
+      return r != kRedo && !L.roomy() && (len > region || (len == region && (r >> 31)));
+    };
+    // (a redo must see this piece's records intact: in_slice kept every write
+    // inside out_w)
+    const bool badA = hasA && overflow(A, rA), badB = hasB && overflow(B, rB);
+    if (__ballot(badA || badB)) {
+      wave_sync();
+      for (uint32_t c = lane; c < (out_bytes + 15u) >> 4; c += kWave) *(u32x4 *)(ws.out_w + 4u * c) = u32x4{0u, 0u, 0u, 0u};
+      wave_sync();
+      rA = kRedo;
+      rB = kRedo;
+    }
+  }
+#endif
   TL(tls + 1);
   if (hasA) ws.len[A.lit] = rA != kRedo ? rA : decode_checked(sm, ws, A.p, A.endbit, A.optr, A.oend);
   if (hasB) ws.len[B.lit] = rB != kRedo ? rB : decode_checked(sm, ws, B.p, B.endbit, B.optr, B.oend);

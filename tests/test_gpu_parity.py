@@ -206,6 +206,53 @@ def test_truncating_capacity(codec, oracle_mod):
         assert status[i] == st
 
 
+def _check_regions(codec, oracle_mod, enc, eoff, cap):
+    out, _, out_len, status = codec.decode(enc, eoff, cap)
+    ref_out, ref_len, ref_st = oracle_mod.decode_batch(enc, eoff, cap, nthreads=8)
+    assert np.array_equal(out_len, ref_len)
+    assert np.array_equal(status, ref_st)
+    starts = cap[:-1].astype(np.int64)
+    lens = ref_len.astype(np.int64)
+    idx = np.repeat(starts, lens) + (np.arange(lens.sum()) - np.repeat(np.cumsum(lens) - lens, lens))
+    assert np.array_equal(out[idx], ref_out[idx])
+    return out, out_len, status
+
+
+def test_decode_exact_and_short_regions(codec, oracle_mod):
+    """Output regions of exactly the plaintext length (a caller that knows the
+    lengths, as a round trip does) decode on the fast loop; regions a byte
+    short or empty truncate as Read does (hc/huffman.go:104: it returns once p
+    is full), as does an INVALID tail behind a region that fills exactly;
+    all mixed in one batch, every literal against the oracle."""
+    from minhq_amd import workloads
+
+    b = workloads.make_batch(40000, "uniform", "hdr", 11, 0, 64)
+    enc_len, enc, eoff = _oracle_encode_batch(oracle_mod, b.data, b.off)
+    plain = np.diff(b.off).astype(np.int64)
+    # exact regions only: the plaintext comes back
+    exact = np.zeros(len(plain) + 1, dtype=np.uint64)
+    exact[1:] = np.cumsum(plain)
+    out, out_len, status = _check_regions(codec, oracle_mod, enc, eoff, exact)
+    assert not status.any() and np.array_equal(out_len.astype(np.int64), plain)
+    assert np.array_equal(out[: len(b.data)], b.data)
+    # mixed: one byte short, empty, roomy, exact; some literals with 32 one
+    # bits after their padding (INVALID, unless their region fills first)
+    rng = np.random.default_rng(5)
+    kind = rng.integers(0, 8, len(plain))
+    lits = [enc[int(eoff[i]): int(eoff[i + 1])].tobytes() for i in range(len(plain))]
+    lits = [x + b"\xff\xff\xff\xff" if k == 7 else x for x, k in zip(lits, kind)]
+    from minhq_amd import hc
+    enc2, eoff2 = hc.pack(lits)
+    region = plain.copy()
+    region = np.where(kind == 0, np.maximum(plain - 1, 0), region)
+    region = np.where(kind == 1, 0, region)
+    region = np.where(kind == 2, (np.diff(eoff2).astype(np.int64) * 8) // 5, region)
+    cap = np.zeros(len(plain) + 1, dtype=np.uint64)
+    cap[1:] = np.cumsum(region)
+    _, _, status = _check_regions(codec, oracle_mod, enc2, eoff2, cap)
+    assert status[kind == 7].sum() == 0  # their regions fill before the ones are read
+
+
 @pytest.mark.parametrize("dist", ["hdr", "print", "adv"])
 def test_config_batches_vs_oracle(codec, oracle_mod, dist):
     from minhq_amd import workloads
