@@ -8,7 +8,8 @@ Write + Pad) on batches that stress the round/mark logic: random bytes (long
 codes), tiny and empty literals (many starts per 16-B chunk), long literals
 beside short ones, unaligned input and output bases, output regions with
 slack, a partial last group, empty regions (the fallback path), and a
-2^20-literal batch, more ranges than the persistent grid's resident waves.
+batch of 1.35 M literals: more ranges than the cooperative kernel's
+resident grid holds.
 """
 import os
 import subprocess
@@ -77,13 +78,14 @@ run(tiny[:9000], slack=nr.integers(0, 4, 9000))
 skip = nr.random(9000) < 0.01
 run(tiny[:9000], skip=skip)
 run([bytes([255] * 4000), b"a", bytes(range(256)) * 7])
-# more ranges than the resident waves (1,024 workgroups x 4 waves): every
-# wave of the persistent grid loops over several ranges
+# more ranges than the cooperative kernel's resident grid holds (1,024
+# workgroups x 4 waves): every wave loops over several ranges
 big = np.random.default_rng(7)
-lens = big.integers(0, 48, 1 << 20)
+nbig = (1 << 20) + 300000
+lens = big.integers(0, 48, nbig)
 blob = big.integers(32, 127, int(lens.sum()), dtype=np.uint8).tobytes()
 cuts = np.concatenate([[0], np.cumsum(lens)])
-run([blob[cuts[i]:cuts[i + 1]] for i in range(1 << 20)], ibias=7, obias=3)
+run([blob[cuts[i]:cuts[i + 1]] for i in range(nbig)], ibias=7, obias=3)
 print("ok")
 '''
 
