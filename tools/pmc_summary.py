@@ -9,7 +9,7 @@ vals = defaultdict(lambda: defaultdict(list))
 for f in sorted(glob.glob(os.path.join(root, "p*", "**", "*counter_collection.csv"), recursive=True)):
     with open(f) as fh:
         for r in csv.DictReader(fh):
-            k = r.get("Kernel_Name", "")
+            k = r.get("Kernel_Name", "").replace("(anonymous namespace)::", "")
             if filt not in k:
                 continue
             vals[k.split("(")[0][-40:]][r["Counter_Name"]].append(float(r["Counter_Value"]))
