@@ -1005,6 +1005,8 @@ extern "C" int mhq_diag_etimeline(unsigned long long *out, int n) {
 hipError_t launch_encode_len(const DevTables &t, const uint8_t *in, const uint64_t *in_off, uint64_t in_bias,
                              uint64_t n, uint32_t *enc_len, hipStream_t s, uint64_t *block_sums) {
   if (n == 0) return hipSuccess;
+  // (one workgroup per group of kLenT literals at full occupancy; a
+  // persistent grid prefetching the next group was slower)
   encode_len_kernel<<<dim3((unsigned)((n + kLenT - 1) / kLenT)), dim3(kLenT), 0, s>>>(in, in_off, in_bias, n,
                                                                                       enc_len, t.len, block_sums);
   return hipGetLastError();

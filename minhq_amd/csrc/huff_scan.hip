@@ -51,6 +51,10 @@ constexpr int kItems = MHQ_SCAN_ITEMS;
 static_assert(kItems % 4 == 0, "whole 16-B loads of lengths");
 constexpr int kChunk = kScanBlock * kItems;
 constexpr int kWaves = kScanBlock / kWave;
+#ifndef MHQ_SCAN_DIRECT_U  // the apply pass's direct-sum loads in flight per thread
+#define MHQ_SCAN_DIRECT_U 16
+#endif
+constexpr int kDirectU = MHQ_SCAN_DIRECT_U;
 
 struct LenVal {  // enc_len -> (bytes, decode capacity)
   const uint32_t *len;
@@ -225,12 +229,21 @@ __global__ __launch_bounds__(kScanBlock) void scan_apply_kernel(F f, uint64_t n,
   if (!sup) {
     // direct form (few sums, see direct_sums): the raw pairs before this
     // chunk's first, added up here; no second pass
+    // (kDirectU loads per thread in flight at once: the pairs are L2 reads,
+    // and one round trip per load was most of this kernel's time)
     typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
-#pragma unroll 4
-    for (uint64_t j = tid; j < first; j += kScanBlock) {
-      const u64x2 v = ((const u64x2 *)sums)[j];
-      pa += v.x;
-      pb += v.y;
+    for (uint64_t j0 = tid; j0 < first; j0 += (uint64_t)kScanBlock * kDirectU) {
+      u64x2 v[kDirectU];
+#pragma unroll
+      for (int u = 0; u < kDirectU; u++) {
+        const uint64_t j = j0 + (uint64_t)u * kScanBlock;
+        v[u] = j < first ? ((const u64x2 *)sums)[j] : u64x2{0ull, 0ull};
+      }
+#pragma unroll
+      for (int u = 0; u < kDirectU; u++) {
+        pa += v[u].x;
+        pb += v[u].y;
+      }
     }
     block_sum2(pa, pb, sh);
   } else {
