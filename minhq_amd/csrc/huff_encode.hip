@@ -77,6 +77,9 @@ __device__ __forceinline__ bool thread_form(uint64_t bytes, uint64_t n) {
   return bytes > (uint64_t)kTinyMean * n && bytes <= (uint64_t)kShortMean * n;
 }
 
+#ifndef MHQ_ENC_QUAD  // the thread kernel puts a staged word's four codes at once when they fit 32 bits
+#define MHQ_ENC_QUAD 1
+#endif
 #ifndef MHQ_ENC_ALIGN  // the thread kernel's LDS alignment (16: its 16-B LDS accesses are single ds_*_b128)
 #define MHQ_ENC_ALIGN 16
 #endif
@@ -183,14 +186,36 @@ __device__ __forceinline__ uint32_t encode_one(Smem<kEmit> &sm, uint32_t p, uint
     uint2 c[4];
 #pragma unroll
     for (int b = 0; b < 4; b++) c[b] = sm.code[(w >> (8 * b)) & 0xffu];
+    uint32_t len[4], code[4];
 #pragma unroll
     for (int b = 0; b < 4; b++) {
       const uint32_t x = q + (uint32_t)b;
       const bool in = x >= p && x < e;
-      const uint32_t len = in ? c[b].y : 0u, code = in ? c[b].x : 0u;
-      bits += len;
-      if (kEmit) bo.put(code, len);
+      len[b] = in ? c[b].y : 0u;
+      code[b] = in ? c[b].x : 0u;
     }
+    const uint32_t l4 = len[0] + len[1] + len[2] + len[3];
+    bits += l4;
+#if MHQ_ENC_QUAD
+    // The word's four codes as one put when they fit 32 bits (text: nearly
+    // always): one LDS OR per word instead of one per byte.
+    if (kEmit) {
+      if (l4 <= 32u) {
+        uint32_t cc = code[0];
+#pragma unroll
+        for (int b = 1; b < 4; b++) cc = (cc << len[b]) | code[b];
+        bo.put(cc, l4);
+      } else {
+#pragma unroll
+        for (int b = 0; b < 4; b++) bo.put(code[b], len[b]);
+      }
+    }
+#else
+    if (kEmit) {
+#pragma unroll
+      for (int b = 0; b < 4; b++) bo.put(code[b], len[b]);
+    }
+#endif
     w = wn;
   }
   if (kEmit) bo.finish();
