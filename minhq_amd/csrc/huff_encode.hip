@@ -77,6 +77,9 @@ __device__ __forceinline__ bool thread_form(uint64_t bytes, uint64_t n) {
   return bytes > (uint64_t)kTinyMean * n && bytes <= (uint64_t)kShortMean * n;
 }
 
+#ifndef MHQ_ENC_PERSIST_MEAN  // the thread kernel's persistent ranges above this mean literal (bytes)
+#define MHQ_ENC_PERSIST_MEAN MHQ_ENC_SHORT_MEAN
+#endif
 #ifndef MHQ_ENC_QUAD  // the thread kernel puts a staged word's four codes at once when they fit 32 bits
 #define MHQ_ENC_QUAD 1
 #endif
@@ -300,7 +303,7 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu((kT / 64 * M
   const uint64_t Ls = min(L0, n);
   uint64_t i_cur = uniform64(vload(in_off, Ls)), o_cur = kEmit ? uniform64(vload(out_off, Ls)) : 0u;
   uint64_t i_end = uniform64(vload(in_off, max(L1, Ls)));
-  if ((bndn - bnd0) > (uint64_t)kShortMean * n) {
+  if ((bndn - bnd0) > (uint64_t)MHQ_ENC_PERSIST_MEAN * n) {
     if (blockIdx.x >= n_persist) return;
     L0 = (uint64_t)blockIdx.x * per_block;
     if (L0 >= n) return;
