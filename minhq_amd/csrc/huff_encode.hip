@@ -44,8 +44,8 @@
 #ifndef MHQ_ENC_BRANCHY  // 1: the bit writer ORs a word out under a per-code branch (0: branch free, config 4 -7 %, config 2 +10 %)
 #define MHQ_ENC_BRANCHY 1
 #endif
-#ifndef MHQ_LEN_U32ROW  // 1: encode_len writes P for every byte of a round as u32 (four 16-B stores per lane)
-#define MHQ_LEN_U32ROW 0
+#ifndef MHQ_LEN_LPL  // encode_len: literals per lane (2: 76 VGPRs, 6 waves per SIMD, 5 % slower)
+#define MHQ_LEN_LPL 1
 #endif
 #ifndef MHQ_ENC_BLOCKS  // resident workgroups per CU
 #define MHQ_ENC_BLOCKS 3
@@ -425,59 +425,6 @@ constexpr int kLenT = kLenSumBlock;  // 4 waves of 64 literals
 constexpr int kLenRB = 4;            // rounds whose loads are issued together
 constexpr uint32_t kRound = kWave * 16;  // bytes per round
 
-// Short literals (every one of the wave's within kPre chunks): one thread per
-// literal, its chunks loaded straight from HBM in one go.
-constexpr int kPre = 5;  // chunks loaded ahead: literals of up to 64 bytes
-
-struct LenAhead {
-  uint64_t a, b;   // byte range (bias removed)
-  u32x4 v[kPre];   // its first kPre chunks
-};
-
-__device__ __forceinline__ void len_load_chunks(LenAhead &t, const uint8_t *__restrict__ in) {
-  const uint64_t c0 = t.a & ~(uint64_t)15;
-  const u32x4 *src = (const u32x4 *)(in + c0);  // aligned chunks holding a valid byte: in bounds
-  const uint64_t nchunks = t.b > t.a ? (t.b - c0 + 15) / 16 : 0;
-#pragma unroll
-  for (int j = 0; j < kPre; j++)
-    if ((uint64_t)j < nchunks) t.v[j] = __builtin_nontemporal_load(src + j);
-}
-
-__device__ __forceinline__ uint32_t len_sum(const LenAhead &t, const uint8_t *__restrict__ in,
-                                            const uint8_t *lens) {
-  const uint64_t a = t.a, b = t.b;
-  uint32_t bits = 0;
-  const uint64_t c0 = a & ~(uint64_t)15;
-  const uint64_t nchunks = b > a ? (b - c0 + 15) / 16 : 0;
-  auto add_chunk = [&](const u32x4 &x, uint64_t c) {
-    const uint32_t w[4] = {x.x, x.y, x.z, x.w};
-    // bytes of this chunk inside [a, b): bits [lo, hi) of m
-    const uint32_t lo = c < a ? (uint32_t)(a - c) : 0u, hi = b - c < 16 ? (uint32_t)(b - c) : 16u;
-    const uint32_t m = ((1u << hi) - 1u) & ~((1u << lo) - 1u);
-#pragma unroll
-    for (int k = 0; k < 16; k++) {
-      const uint32_t l = lens[(w[k >> 2] >> (8 * (k & 3))) & 0xffu];
-      bits = __builtin_amdgcn_ubfe(m, k, 1) * l + bits;
-    }
-  };
-#pragma unroll
-  for (int j = 0; j < kPre; j++)
-    if ((uint64_t)j < nchunks) add_chunk(t.v[j], c0 + 16u * j);
-  // a long literal: the rest in batches of kPre chunks, a batch's loads
-  // issued together (one memory round trip per 80 bytes, not per chunk)
-  const u32x4 *src = (const u32x4 *)(in + c0);
-  for (uint64_t j0 = kPre; j0 < nchunks; j0 += kPre) {
-    u32x4 v[kPre];
-#pragma unroll
-    for (int j = 0; j < kPre; j++)
-      if (j0 + j < nchunks) v[j] = __builtin_nontemporal_load(src + j0 + j);
-#pragma unroll
-    for (int j = 0; j < kPre; j++)
-      if (j0 + j < nchunks) add_chunk(v[j], c0 + 16u * (j0 + j));
-  }
-  return bits;
-}
-
 // Slot of P(x) in a wave's row: lane l's 16 values (4 chunks of 4) go to
 // chunk slots j ^ (l % 4), so the 8 lanes of a ds_write_b128 group spread over
 // the banks (64-B lane stride: linear, lanes l and l+2 collide 4-way).
@@ -497,70 +444,67 @@ __device__ __forceinline__ uint32_t chunk_bits(const u32x4 &x, const uint8_t *le
   return t;
 }
 
-__global__ __launch_bounds__(kLenT) void encode_len_kernel(const uint8_t *__restrict__ in,
-                                                           const uint64_t *__restrict__ in_off, uint64_t in_bias,
-                                                           uint64_t n, uint32_t *__restrict__ enc_len,
-                                                           const uint8_t *__restrict__ g_len,
-                                                           uint64_t *__restrict__ block_sums) {
+// A wave sizes kLenLPL x 64 consecutive literals (lane l: literals l, l + 64,
+// ...), a workgroup of kLenT / kLenLPL threads the kLenT literals of one
+// block sum.  More literals per lane pay a wave's two dependent HBM trips
+// (offsets, then the bytes they locate) less often, but cost registers: the
+// occupancy matters more (layout call).
+constexpr int kLenLPL = MHQ_LEN_LPL;
+constexpr int kLenThreads = kLenT / kLenLPL;
+static_assert(kLenThreads % kWave == 0 && kLenThreads <= 256, "encode_len workgroup shape");
+
+__global__ __launch_bounds__(kLenThreads) void encode_len_kernel(const uint8_t *__restrict__ in,
+                                                                 const uint64_t *__restrict__ in_off,
+                                                                 uint64_t in_bias, uint64_t n,
+                                                                 uint32_t *__restrict__ enc_len,
+                                                                 const uint8_t *__restrict__ g_len,
+                                                                 uint64_t *__restrict__ block_sums) {
   // code lengths one byte each: byte values b and b+1..b+3 share a dword
   // (a broadcast), and only b and b+128 share a bank (ds_read_u8 banks by
   // dword): text lookups are nearly conflict-free, where a u32 table put
   // 0x21 / 0x41 / 0x61 on one bank
+  constexpr int kW = kLenThreads / kWave;
   __shared__ uint8_t lens[256];
-#if MHQ_LEN_U32ROW
-  __shared__ uint32_t pw[kLenT / kWave][kRound + 4];  // P over one round (+ the position after it)
-#else
   // P over one round as chunk prefixes (u32, + the position after the round)
-  // and in-chunk prefixes (u16, at most 15 x 30 bits): two 16-B stores per
-  // lane and round instead of four
-  __shared__ uint32_t ppre[kLenT / kWave][kWave + 4];
-  __shared__ __attribute__((aligned(16))) uint16_t pq[kLenT / kWave][kRound];
-#endif
-  __shared__ uint64_t part[2 * (kLenT / kWave)];
+  // and in-chunk prefixes (u8 or u16, at most 15 x 30 bits): one or two 16-B
+  // stores per lane and round
+  __shared__ uint32_t ppre[kW][kWave + 4];
+  __shared__ __attribute__((aligned(16))) uint16_t pq[kW][kRound];
+  __shared__ uint64_t part[2 * kW];
   const uint32_t lane = threadIdx.x % kWave, wave = threadIdx.x / kWave;
-  const uint64_t s = (uint64_t)blockIdx.x * kLenT + (uint64_t)wave * kWave;  // the wave's first literal
-  const uint64_t i = s + lane;
-  lens[threadIdx.x] = g_len[threadIdx.x];
-  const uint64_t a = in_off[min(i, n) + vzero()] - in_bias;
-  const uint64_t bw = in_off[min(s + kWave, n) + vzero()] - in_bias;  // end of the wave's range
+  const uint64_t s = (uint64_t)blockIdx.x * kLenT + (uint64_t)wave * (kWave * kLenLPL);  // the wave's first literal
+  for (uint32_t x = threadIdx.x; x < 256u; x += kLenThreads) lens[x] = g_len[x];
+  uint64_t a[kLenLPL];
+#pragma unroll
+  for (int k = 0; k < kLenLPL; k++) a[k] = in_off[min(s + (uint64_t)(kWave * k) + lane, n) + vzero()] - in_bias;
+  const uint64_t bw = in_off[min(s + (uint64_t)(kWave * kLenLPL), n) + vzero()] - in_bias;  // the range's end
   __syncthreads();
-  uint32_t el = 0;
+  uint32_t el[kLenLPL] = {};
   if (s < n) {
-    const uint64_t nx = (uint64_t)__shfl_down((unsigned long long)a, 1);  // every lane active: lane 63 is a source
-    const uint64_t b = lane < kWave - 1 ? nx : bw;
-    const uint64_t aw = uniform64(a);  // lane 0: literal s
+    // literal s + 64k + l ends where the next one starts
+    uint64_t b[kLenLPL];
+#pragma unroll
+    for (int k = 0; k < kLenLPL; k++) {
+      const uint64_t nx = (uint64_t)__shfl_down((unsigned long long)a[k], 1);  // every lane active
+      const uint64_t wrap = k + 1 < kLenLPL ? uniform64(a[k + 1 < kLenLPL ? k + 1 : k]) : bw;
+      b[k] = lane < kWave - 1 ? nx : wrap;
+    }
+    const uint64_t aw = uniform64(a[0]);  // lane 0: literal s
     const uint8_t *base8 = in + aw - ((uintptr_t)(in + aw) & 15u);  // pointer arithmetic: global loads, not flat
     const uintptr_t base = (uintptr_t)base8;
     const u32x4 *src = (const u32x4 *)base8;
     // aligned chunks holding a byte of [aw, bw): none for an empty range
     const uint64_t nchunk = bw > aw ? ((uintptr_t)(in + bw) - base + 15u) >> 4 : 0u;
     const uint32_t nround = (uint32_t)((nchunk + kWave - 1) / kWave);
-    // With the byte table and the swizzled P rows the cooperative walk beats
-    // one thread per literal even on short literals (config 2: 18.6 -> 15.9
-    // us); the per-thread form (a wave of literals of at most kPre chunks)
-    // stays behind MHQ_LEN_PER_THREAD.
-#ifdef MHQ_LEN_PER_THREAD
-    const bool lng = b > a && ((uintptr_t)(in + b) - ((uintptr_t)(in + a) & ~(uintptr_t)15) + 15u) / 16u > kPre;
-    if (__ballot(lng) == 0) {
-#else
-    if (false) {
-#endif
-      LenAhead t{};
-      t.a = a;
-      t.b = b;
-      len_load_chunks(t, in);
-      el = (len_sum(t, in, lens) + 7u) >> 3;
-      if (i < n) enc_len[i] = el;
-      goto sums;
+    uint32_t pa[kLenLPL], pb[kLenLPL], Pa[kLenLPL] = {}, Pb[kLenLPL] = {};
+#pragma unroll
+    for (int k = 0; k < kLenLPL; k++) {
+      pa[k] = (uint32_t)((uintptr_t)(in + a[k]) - base);
+      pb[k] = (uint32_t)((uintptr_t)(in + b[k]) - base);
     }
-    const uint32_t pa = (uint32_t)((uintptr_t)(in + a) - base), pb = (uint32_t)((uintptr_t)(in + b) - base);
-#if MHQ_LEN_U32ROW
-    uint32_t *row = pw[wave];
-#else
     uint32_t *pre_row = ppre[wave];
     uint16_t *q_row = pq[wave];
-#endif
-    uint32_t carry = 0, Pa = 0, Pb = 0;
+    uint32_t carry = 0;
     for (uint32_t r0 = 0; r0 < nround; r0 += kLenRB) {
       u32x4 v[kLenRB];
 #pragma unroll
@@ -575,16 +519,6 @@ __global__ __launch_bounds__(kLenT) void encode_len_kernel(const uint8_t *__rest
         uint32_t q[16];
         const uint32_t tot = chunk_bits(v[k], lens, q);
         const uint32_t pre = carry + wave_incl_scan(tot) - tot;
-#if MHQ_LEN_U32ROW
-#pragma unroll
-        for (int j = 0; j < 16; j += 4)
-          *(u32x4 *)(row + prow(16u * lane + j)) = u32x4{pre + q[j], pre + q[j + 1], pre + q[j + 2], pre + q[j + 3]};
-        if (lane == kWave - 1) row[kRound] = pre + tot;
-        wave_sync();
-        const uint32_t lo = (r0 + k) * kRound;  // positions [lo, lo + kRound] are in the row
-        if (pa - lo <= kRound) Pa = row[prow(pa - lo)];
-        if (pb - lo <= kRound) Pb = row[prow(pb - lo)];
-#else
         // When every in-chunk prefix of the round fits a byte (chunks under
         // 16 bits per byte: all text), q is stored as bytes, lane l's 16 at
         // 16 l (one 16-B store; a store group's 8 lanes on 128 consecutive
@@ -606,24 +540,35 @@ __global__ __launch_bounds__(kLenT) void encode_len_kernel(const uint8_t *__rest
         if (lane == kWave - 1) pre_row[kWave] = pre + tot;  // the position after the round
         wave_sync();
         const uint32_t lo = (r0 + k) * kRound;  // positions [lo, lo + kRound]
-        const uint32_t xa = pa - lo, xb = pb - lo;
         const uint8_t *q8 = (const uint8_t *)q_row;
-        if (xa < kRound) Pa = pre_row[xa >> 4] + (bytes ? (uint32_t)q8[xa] : (uint32_t)q_row[xa]);
-        if (xa == kRound) Pa = pre_row[kWave];
-        if (xb < kRound) Pb = pre_row[xb >> 4] + (bytes ? (uint32_t)q8[xb] : (uint32_t)q_row[xb]);
-        if (xb == kRound) Pb = pre_row[kWave];
-#endif
+        auto P = [&](uint32_t x, uint32_t &dst) {
+          if (x < kRound) dst = pre_row[x >> 4] + (bytes ? (uint32_t)q8[x] : (uint32_t)q_row[x]);
+          if (x == kRound) dst = pre_row[kWave];
+        };
+#pragma unroll
+        for (int j = 0; j < kLenLPL; j++) {
+          P(pa[j] - lo, Pa[j]);
+          P(pb[j] - lo, Pb[j]);
+        }
         carry = __builtin_amdgcn_readlane(pre + tot, kWave - 1);
         wave_sync();
       }
     }
-    el = (Pb - Pa + 7u) >> 3;
-    if (i < n) enc_len[i] = el;
+#pragma unroll
+    for (int k = 0; k < kLenLPL; k++) {
+      el[k] = (Pb[k] - Pa[k] + 7u) >> 3;
+      const uint64_t i = s + (uint64_t)(kWave * k) + lane;
+      if (i < n) enc_len[i] = el[k];
+    }
   }
-sums:
   if (!block_sums) return;  // uniform over the grid
   // the block's (sum of enc_len, sum of decode capacities) for the offsets scan
-  uint64_t sa = el, sb = ((uint64_t)el * 8u) / 5u;
+  uint64_t sa = 0, sb = 0;
+#pragma unroll
+  for (int k = 0; k < kLenLPL; k++) {
+    sa += el[k];
+    sb += ((uint64_t)el[k] * 8u) / 5u;
+  }
 #pragma unroll
   for (int d = 1; d < kWave; d <<= 1) {
     sa += __shfl_xor(sa, d);
@@ -637,7 +582,7 @@ sums:
   if (threadIdx.x < 2) {
     uint64_t v = 0;
 #pragma unroll
-    for (int w = 0; w < kLenT / kWave; w++) v += part[2 * w + threadIdx.x];
+    for (int w = 0; w < kW; w++) v += part[2 * w + threadIdx.x];
     block_sums[2 * blockIdx.x + threadIdx.x] = v;
   }
 }
@@ -1035,8 +980,8 @@ hipError_t launch_encode_len(const DevTables &t, const uint8_t *in, const uint64
   if (n == 0) return hipSuccess;
   // (one workgroup per group of kLenT literals at full occupancy; a
   // persistent grid prefetching the next group was slower)
-  encode_len_kernel<<<dim3((unsigned)((n + kLenT - 1) / kLenT)), dim3(kLenT), 0, s>>>(in, in_off, in_bias, n,
-                                                                                      enc_len, t.len, block_sums);
+  encode_len_kernel<<<dim3((unsigned)((n + kLenT - 1) / kLenT)), dim3(kLenThreads), 0, s>>>(in, in_off, in_bias, n,
+                                                                                            enc_len, t.len, block_sums);
   return hipGetLastError();
 }
 
