@@ -322,11 +322,14 @@ inline uint64_t sup_count(uint64_t ns) { return (ns + 1 + kSup - 1) / kSup; }
 // pass, one launch fewer) while that reads at most ~32 MB of L2 in all:
 // nb blocks x ns pairs x 16 B / 2 (at 2^20 literals: the layout call's 513
 // chunks over 4,096 encode_len sums; a scan's own 513 reduce sums).
+#ifndef MHQ_SCAN_DIRECT_LOG2  // the direct form while nb x ns <= 2^this
+#define MHQ_SCAN_DIRECT_LOG2 22
+#endif
 inline bool direct_sums(uint64_t nb, uint64_t ns) {
 #ifdef MHQ_SCAN_NODIRECT  // timing builds: always the three passes
   return false;
 #endif
-  return nb * ns <= (1ull << 22);
+  return nb * ns <= (1ull << MHQ_SCAN_DIRECT_LOG2);
 }
 
 inline size_t run_scan_bytes(uint64_t n) {
