@@ -944,6 +944,9 @@ __device__ void decode_tile_long(const Smem &sm, WaveSmem &ws, const uint8_t *__
     }
   };
   next_lit();
+#ifdef MHQ_X_LONG_NOSTAGE
+  bool staged_once = false;
+#endif
   while (__ballot(have)) {
     // stage: the 8 aligned chunks from the one holding the lane's bit position
     // (the last one holding a byte of the literal at most), by LDS-DMA: wave
@@ -962,6 +965,9 @@ __device__ void decode_tile_long(const Smem &sm, WaveSmem &ws, const uint8_t *__
       p = delta * 8u + (uint32_t)(rel & 7u);
       endw = p + (uint32_t)((ie - ib) * 8u - rel);  // the literal's end in window bits (may lie beyond)
     }
+#ifdef MHQ_X_LONG_NOSTAGE  // timing experiment only (wrong output): windows staged in the first round only
+    if (!staged_once)
+#endif
 #pragma unroll
     for (uint32_t k = 0; k < kWave / 8u; k++) {
       // slot lane % 8 of owner o's window takes chunk (lane % 8) ^ (o % 8)
@@ -973,6 +979,9 @@ __device__ void decode_tile_long(const Smem &sm, WaveSmem &ws, const uint8_t *__
                                          0);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#ifdef MHQ_X_LONG_NOSTAGE
+    staged_once = true;
+#endif
     wave_sync();
     if (have) {
       const bool ends_here = endw + 64u <= kWinBits;

@@ -34,7 +34,10 @@ constexpr uint8_t kDeclared = 4;  // the declared length is not 0
 // H bit, reading no byte at or past limit (hc/io.go:25-55, 73-81).
 // Each block also writes the capacity sums of its strings, per kLenSumBlock,
 // to block_sums: the offsets scan's first pass.
-constexpr int kParsePer = 4;  // strings per parse thread: i = block * kT * kParsePer + k * kT + tid
+#ifndef MHQ_PARSE_PER  // strings per parse / finish thread: i = block * kT * kParsePer + k * kT + tid (1, 4, 8: 1-4 % slower)
+#define MHQ_PARSE_PER 2
+#endif
+constexpr int kParsePer = MHQ_PARSE_PER;
 
 __global__ __launch_bounds__(kT) void read_parse_kernel(const uint8_t *__restrict__ blk, uint64_t blk_len,
                                                         const uint64_t *__restrict__ pos,
