@@ -188,12 +188,30 @@ def kernel_ms(codec, slots, which, launches):
     return events_ms(run, launches)
 
 
-def verify_slot(s, batch=None):
+def decoded_bytes_match(out, cap_off, data, off):
+    """The decoded bytes of every literal (at its capacity offset in `out`)
+    equal the plaintext, compared on the device."""
+    import torch
+
+    lens = off[1:] - off[:-1]
+    total = int(lens.sum().item())
+    if total == 0:
+        return True
+    rep = torch.repeat_interleave(cap_off[:-1] - cap_off[0], lens)
+    within = torch.arange(total, device=lens.device) - torch.repeat_interleave(torch.cumsum(lens, 0) - lens, lens)
+    p0 = int(off[0].item())
+    return torch.equal(out[rep + within], data[p0:p0 + total])
+
+
+def verify_slot(s):
+    """The headline's correctness gate: status, lengths and the decoded bytes
+    of the slot's last round trip."""
     import torch
 
     torch.cuda.synchronize()
     assert int(s.status.sum().item()) == 0, "decode reported INVALID on encoder output"
     assert torch.equal(s.out_len.long(), s.off[1:] - s.off[:-1]), "round trip length mismatch"
+    assert decoded_bytes_match(s.out, s.cap_off, s.data, s.off), "round trip byte mismatch"
 
 
 def decode_algorithmic_bytes(n, enc_bytes, plain_bytes):
@@ -237,33 +255,51 @@ def _threads():
     return _affinity(), "sched_getaffinity"
 
 
-def cpu_baseline(batch, seconds: float):
-    """The oracle (restated Go algorithm) on the host cores: encode + decode,
-    on 1 thread and on the box's thread share; the table-driven decoder
-    beside it (decode only).  Each leg runs for about seconds/4."""
+def _cpu_sample(batch, m):
+    """The first m literals of a batch, encoded by the oracle: (plain bytes,
+    data, off, enc, enc_off, cap_off)."""
     from minhq_amd import hc
     from oracle import oracle
 
-    oracle.build()
-    cores, cores_src = _threads()
-    m = min(batch.n, 1 << 17)
+    m = min(batch.n, m)
     off = batch.off[: m + 1].copy()
-    data = batch.data[: int(off[-1])].copy()
-    plain = int(off[-1])
-    enc_len = oracle.encode_len_batch(data, off, cores)
+    data = batch.data[int(off[0]): int(off[-1])].copy()
+    off -= off[0]
+    enc_len = oracle.encode_len_batch(data, off, _affinity())
     eoff = np.zeros(m + 1, dtype=np.uint64)
     eoff[1:] = np.cumsum(enc_len, dtype=np.uint64)
-    enc = oracle.encode_batch(data, off, eoff, cores)
-    cap = hc.capacity_offsets(eoff)
+    enc = oracle.encode_batch(data, off, eoff, _affinity())
+    return int(off[-1]), data, off, enc, eoff, hc.capacity_offsets(eoff)
 
-    def rate(fn, budget):
-        done, t0 = 0, time.perf_counter()
-        while True:
-            fn()
-            done += 1
-            el = time.perf_counter() - t0
-            if el >= budget:
-                return plain * done / el / GIB, done, el
+
+def _rate(fn, plain, budget):
+    """GiB/s of plaintext of fn() repeated for about `budget` seconds."""
+    done, t0 = 0, time.perf_counter()
+    while True:
+        fn()
+        done += 1
+        el = time.perf_counter() - t0
+        if el >= budget:
+            return round(plain * done / el / GIB, 4), done, round(el, 2)
+
+
+def cpu_baseline(batch, seconds: float):
+    """The oracle (minhq's Go algorithm restated in C) on the host cores, as
+    BASELINE.md asks: config 2 encode+decode on every CPU of this process's
+    affinity (std::thread-style pthreads, one contiguous range of literals
+    each), on the box's OMP_NUM_THREADS share and on one thread; decode legs
+    for the north star and configs 3, 4 and 5 on one thread and on every
+    affinity CPU; the table-driven C decoder beside each.  Bounded samples
+    (first 2^17 literals; config 5 2^15 x 128 B), about `seconds` in all."""
+    from minhq_amd import workloads
+    from oracle import oracle
+
+    oracle.build()
+    allc = _affinity()
+    share, share_src = _threads()
+    leg = max(seconds / 20.0, 0.3)
+    plain, data, off, enc, eoff, cap = _cpu_sample(batch, 1 << 17)
+    m = len(off) - 1
 
     def roundtrip(th):
         def f():
@@ -274,23 +310,36 @@ def cpu_baseline(batch, seconds: float):
             oracle.decode_batch(e, eo, cap, th)
         return f
 
-    leg = max(seconds / 4.0, 0.5)
-    v_all, n_all, t_all = rate(roundtrip(cores), leg)
-    v_one, n_one, t_one = rate(roundtrip(1), leg)
-    f_all, _, _ = rate(lambda: oracle.decode_batch(enc, eoff, cap, cores, fast=True), leg / 2)
-    f_one, _, _ = rate(lambda: oracle.decode_batch(enc, eoff, cap, 1, fast=True), leg / 2)
-    d_all, _, _ = rate(lambda: oracle.decode_batch(enc, eoff, cap, cores), leg / 2)
-    return {"value": round(v_all, 4), "unit": "GiB/s", "cores": cores, "kind": "port",
-            "cores_source": cores_src, "affinity_cpus": _affinity(), "os_cpu_count": os.cpu_count(),
-            "sample": f"first {m} literals of the workload, encode+decode, {n_all} passes in {t_all:.1f}s on "
-                      f"{cores} threads (minhq hc/huffman.go + io/bitio.go bit-serial algorithm restated in C, "
+    v_all, n_all, t_all = _rate(roundtrip(allc), plain, 2 * leg)
+    v_share, _, _ = _rate(roundtrip(share), plain, leg)
+    v_one, n_one, t_one = _rate(roundtrip(1), plain, leg)
+    legs = {}
+    for name, b, mm in (("northstar", workloads.north_star(1 << 17), 1 << 17),
+                        ("config2", batch, 1 << 17),
+                        ("config3", workloads.config3(1 << 17), 1 << 17),
+                        ("config4", workloads.make_batch(1 << 17, "zipf", "hdr", workloads.SEED_ZIPF), 1 << 17),
+                        ("config5", workloads.make_batch(1 << 15, "fixed", "adv", workloads.SEED_ADV, 128, 128),
+                         1 << 15)):
+        pl, _, _, e, eo, co = _cpu_sample(b, mm)
+        legs[name] = {
+            "sample": f"first {min(b.n, mm)} literals ({pl} plaintext bytes)",
+            "restated_go_1_thread": _rate(lambda: oracle.decode_batch(e, eo, co, 1), pl, leg / 2)[0],
+            f"restated_go_{allc}_threads": _rate(lambda: oracle.decode_batch(e, eo, co, allc), pl, leg / 2)[0],
+            f"table_driven_{allc}_threads": _rate(lambda: oracle.decode_batch(e, eo, co, allc, fast=True), pl,
+                                                  leg / 2)[0],
+            "unit": "GiB/s of plaintext (decode)"}
+    return {"value": v_all, "unit": "GiB/s", "cores": allc, "kind": "port",
+            "cores_source": "sched_getaffinity (every CPU this process may run on, BASELINE.md: all nproc cores)",
+            "affinity_cpus": allc, "os_cpu_count": os.cpu_count(),
+            "sample": f"config 2, first {m} literals of the workload, encode+decode, {n_all} passes in {t_all:.1f}s "
+                      f"on {allc} threads (minhq hc/huffman.go + io/bitio.go bit-serial algorithm restated in C, "
                       f"oracle/huff_oracle.c; os.cpu_count()={os.cpu_count()})",
-            "single_thread": {"value": round(v_one, 4), "unit": "GiB/s", "passes": n_one, "seconds": round(t_one, 2)},
-            "decode_only": {"restated_go_all_threads_gib_s": round(d_all, 4),
-                            "table_driven_all_threads_gib_s": round(f_all, 4),
-                            "table_driven_single_thread_gib_s": round(f_one, 4),
-                            "note": "table-driven: a 12-bit LUT per code, tree walk for longer codes and the "
-                                    "literal end (orc_huff_decode_fast); same results as the restated loop"}}
+            "share": {"value": v_share, "threads": share, "threads_source": share_src,
+                      "note": "the GPU box's per-GPU CPU share"},
+            "single_thread": {"value": v_one, "unit": "GiB/s", "passes": n_one, "seconds": t_one},
+            "decode_legs": legs,
+            "note": "table-driven: a 12-bit LUT per code, tree walk for longer codes and the literal end "
+                    "(orc_huff_decode_fast); same results as the restated loop (tests/test_oracle.py)"}
 
 
 class Dev:
@@ -357,12 +406,7 @@ def check_decode(dv, lo, hi, s):
     assert int(s.status[:n].sum().item()) == 0, "INVALID on encoder output"
     lens = (dv.off[lo + 1:hi + 1] - dv.off[lo:hi])
     assert torch.equal(s.out_len[:n].long(), lens), "length mismatch"
-    starts = s.cap_off[:-1]
-    rep = torch.repeat_interleave(starts, lens)
-    within = torch.arange(int(lens.sum().item()), device=lens.device) - torch.repeat_interleave(
-        torch.cumsum(lens, 0) - lens, lens)
-    p0 = int(dv.off[lo].item())
-    assert torch.equal(s.out[rep + within], dv.data[p0:p0 + int(lens.sum().item())]), "byte mismatch"
+    assert decoded_bytes_match(s.out, s.cap_off, dv.data, dv.off[lo:hi + 1]), "byte mismatch"
 
 
 def config4_sharded(codec, dev, world, rank, pg, launches, rotate_bytes):

@@ -304,10 +304,16 @@ __device__ __forceinline__ bool masked_step(const Smem &sm, uint32_t *otgt, BitB
   const uint32_t S = in.top32();
   stop = S >= 0xfffffffcu;
   uint32_t e = sm.lut1[S >> (32 - kLut1Bits)];
-#if !defined(MHQ_X_NOOR)
+#if defined(MHQ_X_NOOR2)  // timing experiment only (wrong output): no OR, the word still computed
+  asm volatile("" ::"v"(pend.v), "v"(pend.ow));
+#elif !defined(MHQ_X_NOOR)
   atomicOr(&otgt[pend.ow], pend.v);
 #endif
+#ifdef MHQ_X_NOREFILL  // timing experiment only (wrong output): the refill word from registers, not LDS
+  const uint32_t w = in.wi * 0x9e3779b9u;
+#else
   const uint32_t w = in.next_word();
+#endif
   bool lng = false;
   if (kLong && ((e == 0u) & !stop)) {  // a code of 13..29 bits (one branch: no short circuit)
     uint32_t sym = 0;
@@ -445,7 +451,7 @@ struct LitRef {
 __device__ unsigned long long g_cnt[8];
 #endif
 #ifdef MHQ_DIAG_TIMELINE  // diagnostic build: per-wave timeline (s_memrealtime, 100 MHz)
-constexpr int kTlSlots = 64;  // per wave: [0] start, [63] end, tile j < 12: 1 + 5j + {0 loads issued, 1 flushed, 2 sorted, 3 loop done, 4 decoded}
+constexpr int kTlSlots = 64;  // per wave: [0] start, [63] end, [56..58] opening, tile j < 11: 1 + 5j + {0 loads issued, 1 flushed, 2 sorted, 3 loop done, 4 decoded}
 __device__ unsigned long long g_tl[1024 * 16 * kTlSlots];
 #define TL(slot)                                                                                          \
   do {                                                                                                    \
@@ -458,6 +464,9 @@ __device__ unsigned long long g_tl[1024 * 16 * kTlSlots];
   do {           \
   } while (0)
 #endif
+// Per-tile stamps of tile j < 11 (slots 1..55; 56..58 hold the opening's
+// stamps, 63 the end); later tiles are not stamped (-1).
+__device__ __forceinline__ int tl_slot(uint32_t j, int k) { return j < 11u ? k + 5 * (int)j : -1; }
 
 // ---- per-wave tiles ------------------------------------------------------
 // Workgroup b owns literals [L0, L1) = [b*R, (b+1)*R); tile t of it is
@@ -599,6 +608,14 @@ template <bool kGaps>
 __device__ __forceinline__ void decode_piece(const Smem &sm, WaveSmem &ws, uint32_t m, uint32_t out_bytes,
                                              uint32_t lane, [[maybe_unused]] int tls = -1) {
   for (uint32_t c = lane; c < (out_bytes + 15u) >> 4; c += kWave) *(u32x4 *)(ws.out_w + 4u * c) = u32x4{0u, 0u, 0u, 0u};
+#ifdef MHQ_X_DBLZERO  // timing experiment: the zeroing twice
+  wave_sync();
+  for (uint32_t c = lane; c < (out_bytes + 15u) >> 4; c += kWave) *(u32x4 *)(ws.out_w + 4u * c) = u32x4{0u, 0u, 0u, 0u};
+#endif
+#ifdef MHQ_X_DBLSORT  // timing experiment: the sort twice
+  for (int rep = 0; rep < 2; rep++)
+#endif
+  {
 #ifdef MHQ_X_NOSORT  // timing experiment only: literals in tile order, lane t on t and 127 - t
   if (lane < m) ws.order[lane] = (uint8_t)lane;
   if (lane + kWave < m) ws.order[lane + kWave] = (uint8_t)(lane + kWave);
@@ -633,6 +650,7 @@ __device__ __forceinline__ void decode_piece(const Smem &sm, WaveSmem &ws, uint3
   }
   wave_sync();
 #endif
+  }
   // Lane t decodes rank t, then rank 127 - t if there is one: the 64 longest
   // literals one per lane, the rest on the lanes with the shortest of those
   // (LPT).  The lane's two fast loops run back to back in one loop (it moves
@@ -736,7 +754,7 @@ __device__ __forceinline__ void decode_piece(const Smem &sm, WaveSmem &ws, uint3
     }
   }
 #endif
-  TL(tls + 1);
+  TL(tls < 0 ? -1 : tls + 1);
   if (hasA) ws.len[A.lit] = rA != kRedo ? rA : decode_checked(sm, ws, A.p, A.endbit, A.optr, A.oend);
   if (hasB) ws.len[B.lit] = rB != kRedo ? rB : decode_checked(sm, ws, B.p, B.endbit, B.optr, B.oend);
   wave_sync();
@@ -1206,6 +1224,14 @@ __global__ __launch_bounds__(kT) void decode_kernel(const uint8_t *__restrict__ 
         const uint32_t c = lane + (uint32_t)kWave * k;
         if (c < chunks) put_chunk(ws, c, tin.v[k]);
       }
+#ifdef MHQ_X_DBLSTAGE  // timing experiment: the staging writes twice
+      wave_sync();
+#pragma unroll
+      for (int k = 0; k < kPF; k++) {
+        const uint32_t c = lane + (uint32_t)kWave * k;
+        if (c < chunks) put_chunk(ws, c, tin.v[k]);
+      }
+#endif
       const uint32_t j0 = 2u * lane;
       if (j0 < cnt) ws.rec[j0] = (uint32_t)(off.i0 - ib + idelta) | (uint32_t)(off.o0 - ob + odelta) << 16;
       if (j0 + 1u < cnt) ws.rec[j0 + 1] = (off.i1 - (uint32_t)ib + idelta) | (off.o1 - (uint32_t)ob + odelta) << 16;
@@ -1216,15 +1242,19 @@ __global__ __launch_bounds__(kT) void decode_kernel(const uint8_t *__restrict__ 
     load_in(tin, in, in_bias, uniform64(off2.i0), uniform64(off2.ie), lane);
     off = off2;
     load_off<kGaps>(off2, in_off, in_end, out_off, L0 + (uint64_t)tile3 * tl, L1, tl, lane);
-    TL(1 + 5 * (int)tl_j);
+    TL(tl_slot(tl_j, 1));
     // the previous tile's output and lengths leave, then this tile decodes
     if (pd_o) {
       store_out(pd_o, (const uint8_t *)ws.out_w, pd_lo, pd_hi, lane);
+#ifdef MHQ_X_DBLFLUSH  // timing experiment: the output flush twice
+      wave_sync();
+      store_out(pd_o, (const uint8_t *)ws.out_w, pd_lo, pd_hi, lane);
+#endif
       flush_lens(ws, pd_s, pd_m, out_len, status, lane);
     }
     pd_o = nullptr;
     wave_sync();
-    TL(2 + 5 * (int)tl_j);
+    TL(tl_slot(tl_j, 2));
     if (fits) {
       if (kGaps) {  // the ends go in the len slots once the previous tile's lengths have left
         const uint32_t j0 = 2u * lane;
@@ -1233,7 +1263,7 @@ __global__ __launch_bounds__(kT) void decode_kernel(const uint8_t *__restrict__ 
         wave_sync();
       }
       const uint32_t out_bytes = ws.rec[cnt] >> 16;
-      decode_piece<kGaps>(sm, ws, cnt, out_bytes, lane, 3 + 5 * (int)tl_j);
+      decode_piece<kGaps>(sm, ws, cnt, out_bytes, lane, tl_slot(tl_j, 3));
       pd_o = oa - odelta;
       pd_lo = odelta;
       pd_hi = out_bytes;
@@ -1253,7 +1283,7 @@ __global__ __launch_bounds__(kT) void decode_kernel(const uint8_t *__restrict__ 
         decode_tile_long<kGaps>(sm, ws, in, in_off, in_end, in_bias, out, out_off, out_bias, out_len, status, s,
                                 cnt, lane);
     }
-    TL(5 + 5 * (int)tl_j);
+    TL(tl_slot(tl_j, 5));
     tl_j++;
     tile = tile2;
     tile2 = tile3;

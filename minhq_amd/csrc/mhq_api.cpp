@@ -94,7 +94,7 @@ struct Device {
   // same stream) may still use them: once the last caller holding one has
   // finished enqueueing (its ScratchLease ends) an event is recorded on the
   // stream, and the buffer is freed when that event has completed (checked
-  // whenever a scratch buffer is handed out), or at mhq_close.
+  // whenever a scratch buffer is handed out or released), or at mhq_close.
   struct Retired {
     void *p;
     hipStream_t s;
@@ -187,14 +187,10 @@ void mark_retired(Device::Retired &r) {
   r.done = ev;
 }
 
-// The scratch buffer of stream s, at least `bytes` long, or null when the
-// context already tracks kMaxScratchStreams streams (the caller then
-// allocates in stream order).  A buffer that has to grow is replaced by a
-// new one and the old one retired (freed at mhq_close): another thread may
-// have just been handed it for work it is still queueing on the same stream.
-void *stream_scratch(Device *d, hipStream_t s, size_t bytes) {
-  std::lock_guard<std::mutex> g(d->scratch_mu);
-  // free the retired buffers whose stream has passed its last use
+// Frees the retired buffers whose stream has passed its last use.  Under
+// scratch_mu; called whenever a scratch buffer is handed out or released, so
+// an outgrown buffer does not stay allocated until mhq_close.
+void reap_retired(Device *d) {
   for (size_t i = 0; i < d->retired.size();) {
     Device::Retired &r = d->retired[i];
     if (r.done && hipEventQuery(r.done) == hipSuccess) {
@@ -206,6 +202,17 @@ void *stream_scratch(Device *d, hipStream_t s, size_t bytes) {
       i++;
     }
   }
+}
+
+// The scratch buffer of stream s, at least `bytes` long, or null when the
+// context already tracks kMaxScratchStreams streams (the caller then
+// allocates in stream order).  A buffer that has to grow is replaced by a
+// new one and the old one retired (freed by reap_retired once its stream has
+// passed it): another thread may have just been handed it for work it is
+// still queueing on the same stream.
+void *stream_scratch(Device *d, hipStream_t s, size_t bytes) {
+  std::lock_guard<std::mutex> g(d->scratch_mu);
+  reap_retired(d);
   for (auto &x : d->scratch) {
     if (x.s != s) continue;
     if (x.bytes >= bytes) {
@@ -246,8 +253,9 @@ void release_scratch(Device *d, void *p) {
     if (r.p == p) {
       r.holders--;
       mark_retired(r);
-      return;
+      break;
     }
+  reap_retired(d);
 }
 
 // stream_scratch for the lifetime of one ABI call.
@@ -308,13 +316,14 @@ int run_chunk(Device *d, Stage &S, const HostJob &j, uint64_t a, uint64_t b) {
   const uint64_t out_bias = j.out_off[a];
   const uint64_t out_bytes = j.out_off[b] - j.out_off[a];
   MHQ_TRY(hipMemcpyAsync(S.out_off.p, j.out_off + a, (m + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, s));
-  // The staging region is zeroed first: the region is copied back whole, and
-  // bytes the kernels leave alone (past a literal's out_len on the decode's
-  // streamed path) would otherwise carry an earlier call's data into the
-  // caller's buffer.  (A device-side fill of at most a few MB per chunk,
-  // hidden behind the chunk's copies.)
+  // A decode's staging region is zeroed first: the region is copied back
+  // whole, and bytes the kernel leaves alone (past a literal's out_len on the
+  // decode's streamed path) would otherwise carry an earlier call's data into
+  // the caller's buffer.  The fill is in stream order, before the kernel (a
+  // few MB per chunk).  Encode needs none: both encode kernels write every
+  // byte of a region (host-path regions are exactly enc_len long).
   uint8_t *dout = (uint8_t *)S.out.p;
-  MHQ_TRY(hipMemsetAsync(dout, 0, out_bytes, s));
+  if (j.op == Op::kDecode) MHQ_TRY(hipMemsetAsync(dout, 0, out_bytes, s));
   const uint64_t *dout_off = (const uint64_t *)S.out_off.p;
   if (j.op == Op::kEncode) {
     MHQ_TRY(mhq::launch_encode(d->tables, din, din_off, in_bias, m, dout, dout_off, out_bias, s));
