@@ -140,10 +140,15 @@ int mhq_huff_decode_dev(mhq_ctx *ctx, int dev, const uint8_t *in, const uint64_t
  * pos[i] (its H bit is bit 7-prefix[i] of that octet) and may use bytes up to
  * limit[i] (the end of its header block: the LimitedReader's underlying EOF
  * truncates the payload silently).  The call writes out_off[0..n] (string i is
- * out[out_off[i] .. out_off[i]+out_len[i]), regions back to back in string
- * order), out_len[i], status[i] and next[i] (the byte after the payload).
- * out_cap must be at least blk_len*8/5 + 1 (enough for any set of
- * non-overlapping literals).  Device pointers; asynchronous on `stream`. */
+ * out[out_off[i] .. out_off[i]+out_len[i]); the regions are disjoint and in
+ * string order), out_len[i], status[i] and next[i] (the byte after the
+ * payload).  When the strings lie in block order (every payload ends at or
+ * before the next string's pos, as in a header block) region i starts at
+ * floor(8*start/5) of its payload start and out_off[n] = floor(8*blk_len/5):
+ * no scan is needed.  Otherwise the regions are laid back to back, each of
+ * floor(8*take/5) (Huffman) or take (raw) bytes.  out_cap must be at least
+ * blk_len*8/5 + 1 (enough for any set of non-overlapping literals).  Device
+ * pointers; asynchronous on `stream`. */
 int mhq_read_strings_dev(mhq_ctx *ctx, int dev, const uint8_t *blk, uint64_t blk_len, const uint64_t *pos,
                          const uint64_t *limit, const uint8_t *prefix, uint64_t n, uint8_t *out, uint64_t out_cap,
                          uint64_t *out_off, uint32_t *out_len, uint8_t *status, uint64_t *next, void *stream);

@@ -56,8 +56,10 @@ hipError_t launch_offsets_pair(const uint32_t *a, const uint32_t *b, uint64_t n,
                                uint64_t *oa, uint64_t *ob, void *scratch, hipStream_t s);
 // launch_offsets_pair over per-kLenSumBlock (sum a, sum b) pairs its producer
 // wrote to block_sums (offsets_sums_scratch_bytes(n) bytes; no reduce pass).
+// With `gate`, the pass does nothing unless *gate == gen when it runs.
 hipError_t launch_offsets_pair_sums(const uint32_t *a, const uint32_t *b, uint64_t n, uint64_t *block_sums,
-                                    uint64_t lim_a, uint64_t lim_b, uint64_t *oa, uint64_t *ob, hipStream_t s);
+                                    uint64_t lim_a, uint64_t lim_b, uint64_t *oa, uint64_t *ob, hipStream_t s,
+                                    const uint64_t *gate = nullptr, uint64_t gen = 0);
 // cap_off[i] = base + sum_{j<i} floor(8*(in_off[j+1]-in_off[j])/5): decode capacities
 // for a batch whose encoded offsets are known.
 // Batch ReadString / WriteStringRaw (str_frame.hip); see include/mhq_huff.h.

@@ -217,7 +217,11 @@ template <class F>
 __global__ __launch_bounds__(kScanBlock) void scan_apply_kernel(F f, uint64_t n, const uint64_t *sums,
                                                                  const uint64_t *sup, uint32_t g, uint64_t base,
                                                                  uint64_t *oa, uint64_t *ob, uint64_t lim_a = ~0ull,
-                                                                 uint64_t lim_b = ~0ull) {
+                                                                 uint64_t lim_b = ~0ull,
+                                                                 const uint64_t *gate = nullptr,
+                                                                 uint64_t gen = 0) {
+  // gated (read_strings): runs only when its producer stored this call's gen
+  if (gate && __builtin_nontemporal_load(gate) != gen) return;
   __shared__ uint64_t sh[2 * kWaves];
   const int tid = threadIdx.x, lane = tid % kWave, wave = tid / kWave;
   // this chunk's items first: their loads are in flight during the prefix
@@ -392,7 +396,8 @@ hipError_t launch_offsets_sums(const uint32_t *enc_len, uint64_t n, uint64_t *bl
 size_t offsets_pair_scratch_bytes(uint64_t n) { return run_scan_bytes(n); }
 
 hipError_t launch_offsets_pair_sums(const uint32_t *a, const uint32_t *b, uint64_t n, uint64_t *block_sums,
-                                    uint64_t lim_a, uint64_t lim_b, uint64_t *oa, uint64_t *ob, hipStream_t s) {
+                                    uint64_t lim_a, uint64_t lim_b, uint64_t *oa, uint64_t *ob, hipStream_t s,
+                                    const uint64_t *gate, uint64_t gen) {
   const uint64_t nb = (n + 1 + kChunk - 1) / kChunk;
   const uint64_t ns = (n + kLenSumBlock - 1) / kLenSumBlock;
   const uint64_t nsup = sup_count(ns);
@@ -401,7 +406,7 @@ hipError_t launch_offsets_pair_sums(const uint32_t *a, const uint32_t *b, uint64
   if (!direct) scan_sums_kernel<<<dim3((unsigned)nsup), dim3(kScanBlock), 0, s>>>(block_sums, ns, sup);
   scan_apply_kernel<PairVal><<<dim3((unsigned)nb), dim3(kScanBlock), 0, s>>>(
       PairVal{a, b, n}, n, block_sums, direct ? nullptr : sup, (uint32_t)(kChunk / kLenSumBlock), 0, oa, ob, lim_a,
-      lim_b);
+      lim_b, gate, gen);
   return hipGetLastError();
 }
 

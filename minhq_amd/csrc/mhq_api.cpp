@@ -10,6 +10,7 @@
 // Offsets are rebased with a per-chunk bias instead of being rewritten.
 // Device-resident entry points only enqueue kernels on the caller's stream.
 #include <hip/hip_runtime.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -64,8 +65,16 @@ struct Buffer {
 #define MHQ_HOST_LEN_CHUNK_MB 2
 #endif
 constexpr int kPipe = MHQ_HOST_PIPE;  // streams (and staging sets) per device for host-memory calls
-constexpr uint64_t kChunkBytes = (uint64_t)MHQ_HOST_CHUNK_MB << 20;  // input bytes per pipelined chunk
-constexpr uint64_t kLenChunkBytes = (uint64_t)MHQ_HOST_LEN_CHUNK_MB << 20;
+// input bytes per pipelined chunk (the environment's MHQ_HOST_CHUNK_MB /
+// MHQ_HOST_LEN_CHUNK_MB override the built-in sizes: tuning and the
+// host-path experiments of tools/hostpath.py)
+uint64_t env_mb(const char *name, uint64_t dflt) {
+  const char *e = getenv(name);
+  const long v = e ? atol(e) : 0;
+  return (v > 0 && v <= 1024 ? (uint64_t)v : dflt) << 20;
+}
+const uint64_t kChunkBytes = env_mb("MHQ_HOST_CHUNK_MB", MHQ_HOST_CHUNK_MB);
+const uint64_t kLenChunkBytes = env_mb("MHQ_HOST_LEN_CHUNK_MB", MHQ_HOST_LEN_CHUNK_MB);
 
 struct Stage {
   hipStream_t s = nullptr;

@@ -11,6 +11,8 @@
 // are integer/byte work with one thread per string.
 #include <hip/hip_runtime.h>
 
+#include <atomic>
+
 #include "huff_common.h"
 #include "huff_kernels.h"
 
@@ -39,17 +41,28 @@ constexpr uint8_t kDeclared = 4;  // the declared length is not 0
 #endif
 constexpr int kParsePer = MHQ_PARSE_PER;
 
+// Output regions (see launch_read_strings): string i's region starts at
+// floor(8 * start_i / 5), its payload start scaled by the Huffman bound.  When
+// the strings lie in block order (every payload ends at or before the next
+// string's pos) these regions are disjoint, ordered and each holds
+// floor(8 * take_i / 5) bytes, so no scan is needed; the kernel writes them
+// to out_off and, if some string is out of order, stores `gen` to *order_bad
+// (the scan's apply pass then lays the regions out back to back instead).
+__device__ __forceinline__ uint64_t scaled(uint64_t x) { return x / 5u * 8u + (x % 5u) * 8u / 5u; }
+
 __global__ __launch_bounds__(kT) void read_parse_kernel(const uint8_t *__restrict__ blk, uint64_t blk_len,
                                                         const uint64_t *__restrict__ pos,
                                                         const uint64_t *__restrict__ limit,
                                                         const uint8_t *__restrict__ prefix, uint64_t n,
                                                         ReadScratch sc, uint64_t *__restrict__ next,
-                                                        uint64_t *__restrict__ block_sums) {
+                                                        uint64_t *__restrict__ block_sums,
+                                                        uint64_t *__restrict__ out_off, uint64_t *order_bad,
+                                                        uint64_t gen) {
   static_assert(kT == kLenSumBlock, "block sums per kLenSumBlock strings: one per k");
   // Every load of the thread's strings is issued before the first one is
   // used (the per-string chain pos -> header octet is two dependent loads).
   const uint64_t i0 = (uint64_t)blockIdx.x * (kT * kParsePer) + threadIdx.x;
-  uint64_t p0[kParsePer], lim[kParsePer];
+  uint64_t p0[kParsePer], lim[kParsePer], pn[kParsePer];
   uint32_t pf[kParsePer], b0[kParsePer];
 #pragma unroll
   for (int k = 0; k < kParsePer; k++) {
@@ -58,10 +71,12 @@ __global__ __launch_bounds__(kT) void read_parse_kernel(const uint8_t *__restric
     p0[k] = pos[j];
     lim[k] = min(limit[j], blk_len);  // a limit past the block is the block's end: no byte past blk_len is read
     pf[k] = prefix[j];
+    pn[k] = i + 1 < n ? pos[i + 1] : blk_len;  // the next string's pos (order test)
   }
 #pragma unroll
   for (int k = 0; k < kParsePer; k++) b0[k] = p0[k] < lim[k] ? blk[p0[k]] : 0u;
   uint32_t caps[kParsePer];
+  bool bad = false;
 #pragma unroll
   for (int k = 0; k < kParsePer; k++) {
     const uint64_t i = i0 + (uint64_t)k * kT;
@@ -108,7 +123,14 @@ __global__ __launch_bounds__(kT) void read_parse_kernel(const uint8_t *__restric
     caps[k] = kind == 1 ? (uint32_t)(take * 8 / 5) : (uint32_t)take;
     sc.cap[i] = caps[k];
     next[i] = kind == 2 ? p0[k] : start + take;
+    // the region at the scaled payload start; in block order the next one
+    // starts at or after scaled(start + take) (its payload starts after its
+    // pos, which is at or after this payload's end)
+    out_off[i] = scaled(start);
+    if (i == n - 1) out_off[n] = scaled(blk_len);
+    bad |= start + take > min(pn[k], blk_len);
   }
+  if (bad) *order_bad = gen;  // (rare: every writer stores the same value)
   // (sum of cap, sum of cap) per kLenSumBlock strings: group k of this block
   __shared__ uint64_t part[kParsePer][kT / 64];
   const uint32_t lane = threadIdx.x % 64, wave = threadIdx.x / 64;
@@ -500,7 +522,7 @@ namespace {
 
 // read_strings' scratch, 16-B aligned pieces of one allocation.
 struct ReadLayout {
-  size_t start, hend, cap, kind, sums, total;
+  size_t start, hend, cap, kind, order_bad, sums, total;
   ReadLayout(uint64_t n, uint64_t blk_len) {
     size_t o = 0;
     auto take_ = [&](size_t bytes) {
@@ -512,6 +534,7 @@ struct ReadLayout {
     hend = take_(8 * n);
     cap = take_(4 * n);
     kind = take_(n);
+    order_bad = take_(8);
     sums = take_(offsets_sums_scratch_bytes(n));
     total = o;
   }
@@ -521,9 +544,14 @@ struct ReadLayout {
 
 size_t read_strings_scratch_bytes(uint64_t n, uint64_t blk_len) { return ReadLayout(n, blk_len).total; }
 
-// parse (+ block sums) -> one scan of the capacities into out_off, clamped to
-// the output -> decode of the Huffman payloads where they lie in the block
-// (launch_decode with in_end) -> finish.
+// parse (+ block sums, + the output regions at the scaled payload starts) ->
+// only if some string lies out of block order: one scan of the capacities
+// into out_off (regions back to back), clamped to the output -> decode of the
+// Huffman payloads where they lie in the block (launch_decode with in_end) ->
+// finish.  The scan's apply pass is always launched but returns at once
+// unless parse stored this call's generation number to order_bad (a number
+// no earlier call used: no reset, and stale scratch contents can only cause
+// the always-correct scan).
 hipError_t launch_read_strings(const DevTables &t, const uint8_t *blk, uint64_t blk_len, const uint64_t *pos,
                                const uint64_t *limit, const uint8_t *prefix, uint64_t n, uint8_t *out,
                                uint64_t out_cap, uint64_t *out_off, uint32_t *out_len, uint8_t *status,
@@ -542,12 +570,17 @@ hipError_t launch_read_strings(const DevTables &t, const uint8_t *blk, uint64_t 
     e = (x);                     \
     if (e != hipSuccess) goto done; \
   } while (0)
-  read_parse_kernel<<<(unsigned)((n + kT * kParsePer - 1) / (kT * kParsePer)), kT, 0, s>>>(blk, blk_len, pos, limit, prefix, n, sc, next,
-                                             (uint64_t *)(base + L.sums));
-  TRY(hipGetLastError());
-  // output regions: capacities back to back
-  TRY(launch_offsets_pair_sums(sc.cap, nullptr, n, (uint64_t *)(base + L.sums), out_cap, out_cap, out_off, nullptr,
-                               s));
+  {
+    static std::atomic<uint64_t> g_gen{0};
+    const uint64_t gen = 0x6d68712000000000ull + g_gen.fetch_add(1, std::memory_order_relaxed) + 1;
+    uint64_t *order_bad = (uint64_t *)(base + L.order_bad);
+    read_parse_kernel<<<(unsigned)((n + kT * kParsePer - 1) / (kT * kParsePer)), kT, 0, s>>>(
+        blk, blk_len, pos, limit, prefix, n, sc, next, (uint64_t *)(base + L.sums), out_off, order_bad, gen);
+    TRY(hipGetLastError());
+    // strings out of block order: capacities back to back instead
+    TRY(launch_offsets_pair_sums(sc.cap, nullptr, n, (uint64_t *)(base + L.sums), out_cap, out_cap, out_off,
+                                 nullptr, s, order_bad, gen));
+  }
   TRY(launch_decode(t, blk, sc.start, 0, n, out, out_off, 0, out_len, status, s, sc.hend));
   read_finish_kernel<<<(unsigned)((n + kT * kParsePer - 1) / (kT * kParsePer)), kT, 0, s>>>(blk, sc, n, out_off, next, out, out_len, status, out_cap);
   TRY(hipGetLastError());

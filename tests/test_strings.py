@@ -273,3 +273,55 @@ def test_read_wild_pos_and_reverse_order_at_buffer_end(codec, oracle_mod):
         got = o[int(oo[k]): int(oo[k]) + int(ol[k])].tobytes()
         assert (got, int(s_h[k])) == (ref, _oracle_status(rc)), (k, q)
         assert int(nx[k]) == q + used, (k, q)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("order", ["block", "reversed"])
+def test_read_regions_layout(codec, oracle_mod, order):
+    """The output regions of mhq_read_strings_dev: in block order each starts
+    at floor(8*start/5) of its payload start (no scan) and out_off[n] =
+    floor(8*blk_len/5); out of block order they lie back to back, each of
+    the string's capacity.  Either way disjoint, in string order, and every
+    string equals the oracle's."""
+    import numpy as np
+    import torch
+
+    rng = random.Random(77 if order == "block" else 78)
+    strs = _random_strings(rng, 5000)
+    blk, pos = bytearray(), []
+    for s in strs:
+        if rng.random() < 0.3:
+            blk += b"\x82"  # another instruction's octet between two fields
+        pos.append(len(blk))
+        blk += oracle_mod.write_string(s, prefix=7, choice=rng.choice([1, 1, 2]))
+    blk = bytes(blk)
+    P = pos if order == "block" else list(reversed(pos))
+    n, L = len(P), len(blk)
+    dev = torch.device("cuda:0")
+    t_blk = torch.frombuffer(bytearray(blk), dtype=torch.uint8).to(dev)
+    t_pos = torch.tensor(np.asarray(P, dtype=np.int64), device=dev)
+    t_lim = torch.full((n,), L, dtype=torch.int64, device=dev)
+    t_pf = torch.full((n,), 7, dtype=torch.uint8, device=dev)
+    out = torch.zeros(L * 8 // 5 + 16, dtype=torch.uint8, device=dev)
+    out_off = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+    out_len = torch.zeros(n, dtype=torch.int32, device=dev)
+    st = torch.zeros(n, dtype=torch.uint8, device=dev)
+    nxt = torch.zeros(n, dtype=torch.int64, device=dev)
+    codec.read_strings_dev(t_blk, t_pos, t_lim, t_pf, out, out_off, out_len, st, nxt)
+    torch.cuda.synchronize()
+    o, oo, ol = out.cpu().numpy(), out_off.cpu().numpy(), out_len.cpu().numpy()
+    assert (np.diff(oo) >= 0).all()
+    for k, q in enumerate(P):
+        ref, rc, used = oracle_mod.read_string(blk[q:], prefix=7)
+        assert o[oo[k]:oo[k] + ol[k]].tobytes() == ref and int(st[k]) == _oracle_status(rc), k
+        assert int(nxt[k]) == q + used
+        take, _, hdr = oracle_mod.read_int(blk[q:], 7, skip_bits=1)
+        start = q + hdr
+        cap = take * 8 // 5 if blk[q] & 0x80 else take
+        if order == "block":
+            assert oo[k] == start * 8 // 5, k
+        assert oo[k] + cap <= oo[k + 1], k
+        if order != "block":
+            assert oo[k + 1] - oo[k] == cap, k
+    if order == "block":
+        assert oo[n] == L * 8 // 5

@@ -1,0 +1,96 @@
+#!/usr/bin/env python3
+"""Host-memory (PCIe-inclusive) decode rate before and after the things a
+long-lived caller does in between (a later decode in the
+same process ran at 5-9 GiB/s instead of 23-24).
+
+    python tools/hostpath.py [--steps a,b,...]
+
+Times mhq_huff_decode of the config-2 batch (pinned input and outputs) three
+times, then runs each disturbance in turn and times the decode again after
+it.  Disturbances:
+  devalloc  8 GiB of device memory allocated, touched and freed (torch, then
+            empty_cache)
+  pinalloc  2 GiB of pinned host memory allocated, touched and freed
+  bigdec    config 5's host decode (4 x 2^20 x 128 B adversarial literals)
+  lenbig    encode_len of the batch with 16 MB chunks (MHQ_HOST_LEN_CHUNK_MB
+            is read once per process: run with it set in the environment)
+  encode    the host encode (encode_len + host scan + encode) of the batch
+  newctx    a second context opened, used and closed
+Prints one JSON line: GiB/s per measurement, in order.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--steps", default="devalloc,pinalloc,encode,lenbig,bigdec,newctx")
+    args = ap.parse_args()
+    import torch
+
+    import bench
+    from minhq_amd import hc, workloads
+
+    codec = hc.Codec(devices=[0])
+    b = workloads.make_batch(1 << 20, "uniform", "hdr", workloads.SEED_NORTH_STAR, 8, 64, "config2")
+    pin = lambda a: torch.from_numpy(a).pin_memory().numpy()  # noqa: E731
+    data, off = pin(b.data), pin(b.off)
+    epool, dpool = bench.PinnedPool(), bench.PinnedPool()
+    enc, eoff = codec.encode(data, off, alloc=epool)
+    enc, eoff = pin(np.array(enc)), pin(np.array(eoff))
+    cap = pin(hc.capacity_offsets(eoff))
+
+    def dec():
+        dpool.rewind()
+        t0 = time.perf_counter()
+        _, _, out_len, st = codec.decode(enc, eoff, cap, alloc=dpool)
+        t1 = time.perf_counter()
+        assert not st.any() and np.array_equal(out_len.astype(np.uint64), np.diff(b.off))
+        return round(b.nbytes / (t1 - t0) / (1 << 30), 2)
+
+    res = {"first": [dec() for _ in range(4)]}
+    for step in args.steps.split(","):
+        t0 = time.perf_counter()
+        if step == "devalloc":
+            x = torch.empty(8 << 30, dtype=torch.uint8, device="cuda")
+            x.fill_(1)
+            torch.cuda.synchronize()
+            del x
+            torch.cuda.empty_cache()
+        elif step == "pinalloc":
+            x = torch.empty(2 << 30, dtype=torch.uint8).pin_memory()
+            x.fill_(1)
+            del x
+        elif step == "bigdec":
+            c5 = workloads.make_batch(4 << 20, "fixed", "adv", workloads.SEED_ADV, 128, 128)
+            e5, o5 = codec.encode(c5.data, c5.off)
+            codec.decode(e5, o5)
+            del c5, e5, o5
+        elif step == "lenbig":
+            codec.encode_len(data, off)
+        elif step == "encode":
+            epool.rewind()
+            codec.encode(data, off, alloc=epool)
+        elif step == "newctx":
+            with hc.Codec(devices=[0]) as c2:
+                c2.decode(enc, eoff, cap)
+        else:
+            raise SystemExit(f"unknown step {step}")
+        took = round(time.perf_counter() - t0, 2)
+        res[step] = {"after": [dec() for _ in range(3)], "step_s": took}
+        print(step, res[step], file=sys.stderr, flush=True)
+    res["env"] = {k: os.environ.get(k) for k in ("MHQ_HOST_CHUNK_MB", "MHQ_HOST_LEN_CHUNK_MB")}
+    print(json.dumps(res), flush=True)
+
+
+if __name__ == "__main__":
+    main()
