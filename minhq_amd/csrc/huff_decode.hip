@@ -350,6 +350,91 @@ __device__ __forceinline__ bool masked_step(const Smem &sm, uint32_t *otgt, BitB
   return stop || !ok;
 }
 
+#ifndef MHQ_DEC_LEAN  // 1: the lean fast loop (LDS pointers, no per-step crossing mask)
+#define MHQ_DEC_LEAN 1
+#endif
+// The lean form of the fast loop's state: the output word and the next
+// stream word are held as LDS pointers (their addresses need no arithmetic
+// per step), and a step's output word is OR-ed whether or not a code crossed
+// the literal's end -- a crossing makes the whole piece be decoded again by
+// the checked loop over a re-zeroed output region (decode_piece), so stray
+// bits of a malformed literal never survive.
+struct OutAccL {
+  uint64_t acc;
+  uint32_t ab;
+  uint32_t *op;  // the word being filled
+  __device__ __forceinline__ void init(uint32_t *out_w, uint32_t optr) {
+    acc = 0;
+    op = out_w + (optr >> 2);
+    ab = (optr & 3u) * 8u;
+  }
+  __device__ __forceinline__ void put(uint32_t syms, uint32_t nbits) {
+    acc |= (uint64_t)syms << ab;
+    ab += nbits;
+  }
+  __device__ __forceinline__ uint32_t optr(const uint32_t *out_w) const {
+    return (uint32_t)(op - out_w) * 4u + (ab >> 3);
+  }
+};
+struct BitBufL {  // BitBufM with the next word by pointer
+  uint64_t bb;
+  int32_t left, rem;
+  const uint32_t *wp;
+  __device__ __forceinline__ void init(const uint32_t *words, uint32_t p0, uint32_t endbit) {
+    const uint32_t k = p0 >> 5;
+    const int32_t e = (int32_t)endbit - (int32_t)(32u * k);
+    const uint32_t w0 = words[k] | ones_past(e), w1 = words[k + 1] | ones_past(e - 32);
+    bb = (((uint64_t)w0 << 32) | w1) << (p0 & 31u);
+    rem = e - 64;
+    wp = words + k + 2u;
+    left = (int32_t)(endbit - p0);
+  }
+  __device__ __forceinline__ void refill(uint32_t w) {
+    const int32_t nb = left - rem;  // kb - p
+    const bool need = nb <= 32;
+    bb |= (uint64_t)(need ? (w | ones_past(rem)) : 0u) << ((uint32_t)(32 - nb) & 63u);
+    rem -= need ? 32 : 0;
+    wp += need ? 1 : 0;
+  }
+  __device__ __forceinline__ uint32_t top32() const { return (uint32_t)(bb >> 32); }
+  __device__ __forceinline__ void consume(uint32_t e) {
+    bb <<= (e & 63u);
+    left -= (int32_t)(e & 0xffu);
+  }
+};
+struct PendL {
+  uint32_t *p, v;
+};
+template <bool kLong = true>
+__device__ __forceinline__ bool masked_step_lean(const Smem &sm, BitBufL &in, OutAccL &out, PendL &pend, bool &stop) {
+  const uint32_t S = in.top32();
+  stop = S >= 0xfffffffcu;
+  uint32_t e = sm.lut1[S >> (32 - kLut1Bits)];
+  atomicOr(pend.p, pend.v);
+  const uint32_t w = *in.wp;
+  bool lng = false;
+  if (kLong && ((e == 0u) & !stop)) {  // a code of 13..29 bits (one branch: no short circuit)
+    uint32_t sym = 0;
+    const uint32_t L = long_code(sm.lut2, S, sym);
+    e = L | (8u << 8) | (sym << 16);
+    lng = true;
+  }
+  out.put(e >> 16, (e >> 8) & 0xffu);
+  in.consume(e);
+  uint32_t e2 = sm.lut1[in.top32() >> (32 - kLut1Bits)];
+  e2 = lng ? 0u : e2;
+  out.put(e2 >> 16, (e2 >> 8) & 0xffu);
+  in.consume(e2);
+  in.refill(w);
+  pend.p = out.op;
+  pend.v = (uint32_t)out.acc;
+  const uint32_t t = out.ab & 32u;
+  out.acc >>= t;
+  out.op += t >> 5;
+  out.ab &= 31u;
+  return stop || in.left < 0;
+}
+
 // BitBuf over a long-path window (LDS-DMA): words left in memory byte order
 // (each is byte-swapped as it is read), and the window's 16-B chunks stored
 // XOR-swizzled: chunk c of lane l's window sits in slot c ^ (l % 8), so word k
@@ -681,6 +766,40 @@ __device__ __forceinline__ void decode_piece(const Smem &sm, WaveSmem &ws, uint3
   const bool roomA = hasA && (A.roomy() || (MHQ_DEC_OPTIMISTIC && A.in_slice()));
   const bool roomB = hasB && (B.roomy() || (MHQ_DEC_OPTIMISTIC && B.in_slice()));
   uint32_t rA = kRedo, rB = kRedo;
+#if MHQ_DEC_LEAN
+  bool crossed = false;  // a code crossed a literal's end: the piece is redone (stray output bits)
+  {
+    BitBufL in, inB;  // inB: B's stream, set up once for the in-loop switch
+    in.init(ws.in_w, roomA ? A.p : B.p, roomA ? A.endbit : B.endbit);
+    inB.init(ws.in_w, B.p, B.endbit);
+    OutAccL out;
+    out.init(ws.out_w, roomA ? A.optr : B.optr);
+    uint32_t ost = roomA ? ostartA : ostartB;
+    PendL pend{out.op, 0u};
+    bool onB = !roomA, active = roomA || roomB;
+    while (active) {
+      bool stop;
+#pragma unroll
+      for (int k = 1; k < MHQ_DEC_STEPS; k++) masked_step_lean<MHQ_DEC_LONG1 != 0>(sm, in, out, pend, stop);
+      if (masked_step_lean(sm, in, out, pend, stop)) {
+        // stop: the EOS prefix (INVALID when a 31st bit of the literal follows);
+        // left < 0: a code crossed the end
+        const bool cr = in.left < 0;
+        crossed |= cr;
+        const uint32_t r = cr ? kRedo : (out.optr(ws.out_w) - ost) | ((uint32_t)(in.left > kEosOnes) << 31);
+        rA = onB ? rA : r;
+        rB = onB ? r : rB;
+        active = !onB && roomB;
+        in = inB;  // (unused unless active)
+        out.init(ws.out_w, B.optr);
+        ost = ostartB;
+        onB = true;
+      }
+    }
+    atomicOr(pend.p, pend.v);
+  }
+#else
+  constexpr bool crossed = false;
   {
     BitBufM in, inB;  // inB: B's stream, set up once for the in-loop switch
     in.init(ws.in_w, roomA ? A.p : B.p, roomA ? A.endbit : B.endbit);
@@ -730,7 +849,8 @@ __device__ __forceinline__ void decode_piece(const Smem &sm, WaveSmem &ws, uint3
     atomicOr(&ws.out_w[pend.ow], pend.v);
 #endif
   }
-#if MHQ_DEC_OPTIMISTIC
+#endif
+#if MHQ_DEC_OPTIMISTIC || MHQ_DEC_LEAN
   {
     // A fast result for a region that can truncate stands when it fits: a
     // longer output has run past the region into a neighbour's bytes, and an
@@ -744,8 +864,9 @@ __device__ __forceinline__ void decode_piece(const Smem &sm, WaveSmem &ws, uint3
     };
     // (a redo must see this piece's records intact: in_slice kept every write
     // inside out_w)
-    const bool badA = hasA && overflow(A, rA), badB = hasB && overflow(B, rB);
-    if (__ballot(badA || badB)) {
+    const bool badA = hasA && MHQ_DEC_OPTIMISTIC && overflow(A, rA);
+    const bool badB = hasB && MHQ_DEC_OPTIMISTIC && overflow(B, rB);
+    if (__ballot(badA || badB || crossed)) {
       wave_sync();
       for (uint32_t c = lane; c < (out_bytes + 15u) >> 4; c += kWave) *(u32x4 *)(ws.out_w + 4u * c) = u32x4{0u, 0u, 0u, 0u};
       wave_sync();

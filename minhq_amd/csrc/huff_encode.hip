@@ -53,6 +53,9 @@
 #ifndef MHQ_ENC_SHORT_MEAN  // mean plaintext bytes up to which a workgroup takes one range of kT literals
 #define MHQ_ENC_SHORT_MEAN 40
 #endif
+#ifndef MHQ_ENC_SHORT_GENS  // resident generations of the short form's grid before its workgroups loop over ranges
+#define MHQ_ENC_SHORT_GENS 4
+#endif
 #ifndef MHQ_ENC_TINY_MEAN  // mean plaintext bytes up to which the cooperative kernel encodes (per-literal costs)
 #define MHQ_ENC_TINY_MEAN 20
 #endif
@@ -297,13 +300,17 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu((kT / 64 * M
   // sub-tiles stay full) in the first workgroups, the others ending at once.
   // The short form's offsets are loaded beside the batch's bounds (its bytes
   // only once the form is known: a workgroup that ends at once loads nothing).
+  // (A grid capped below ceil(n / kT) -- huge batches, so that the launch of
+  // the form the batch does not take stays small -- makes the short form's
+  // workgroups take ranges blockIdx.x + k * gridDim.x in turn.)
   const uint64_t bnd0 = in_off[0], bndn = in_off[n];
   uint64_t L0 = (uint64_t)blockIdx.x * kT;
   uint64_t L1 = min(L0 + (uint64_t)kT, n);
   const uint64_t Ls = min(L0, n);
   uint64_t i_cur = uniform64(vload(in_off, Ls)), o_cur = kEmit ? uniform64(vload(out_off, Ls)) : 0u;
   uint64_t i_end = uniform64(vload(in_off, max(L1, Ls)));
-  if ((bndn - bnd0) > (uint64_t)MHQ_ENC_PERSIST_MEAN * n) {
+  const bool persist = (bndn - bnd0) > (uint64_t)MHQ_ENC_PERSIST_MEAN * n;
+  if (persist) {
     if (blockIdx.x >= n_persist) return;
     L0 = (uint64_t)blockIdx.x * per_block;
     if (L0 >= n) return;
@@ -322,7 +329,20 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu((kT / 64 * M
   uint32_t pd_lo = 0, pd_hi = 0;
   bool pending = false;
 
-  while (cur < L1) {
+  for (;;) {
+  if (cur >= L1) {
+    // the short form's next range (a capped grid), its first sub-tile's loads issued now
+    if (persist || L1 >= n) break;
+    L0 += (uint64_t)gridDim.x * kT;
+    if (L0 >= n) break;
+    L1 = min(L0 + (uint64_t)kT, n);
+    __syncthreads();  // in_w free
+    i_cur = uniform64(vload(in_off, L0));
+    o_cur = kEmit ? uniform64(vload(out_off, L0)) : 0u;
+    i_end = uniform64(vload(in_off, L1));
+    issue_next<kEmit>(nx, in, in_bias, in_off, out_off, L0, L1, i_cur, i_end, tid);
+    cur = L0;
+  }
     // consume the prefetch (the previous sub-tile ended with a barrier: in_w is free)
     const uint32_t cnt = (uint32_t)min((uint64_t)kT, L1 - cur);
     const uint32_t ie = (uint32_t)(nx.ie64 - i_cur), oe = kEmit ? (uint32_t)(nx.oe64 - o_cur) : 0u;
@@ -1011,7 +1031,12 @@ hipError_t launch_encode(const DevTables &t, const uint8_t *in, const uint64_t *
     // persistent form: MHQ_ENC_BLOCKS resident workgroups per CU (never more than the tiles)
     const unsigned persist = dev::tile_grid((n + kT - 1) / kT, 1, MHQ_ENC_BLOCKS * MHQ_PER_CU);
     const uint64_t tiles = (n + kT - 1) / kT;
-    const unsigned grid = (unsigned)(tiles > persist ? tiles : persist);
+    // short form: one range of kT literals per workgroup, at most kShortGen
+    // resident generations of workgroups (past that they loop over ranges), so
+    // that for a batch the cooperative kernel takes this launch stays small
+    const uint64_t cap = (uint64_t)persist * MHQ_ENC_SHORT_GENS;
+    const uint64_t want = tiles < cap ? tiles : cap;
+    const unsigned grid = (unsigned)(want > persist ? want : persist);
     encode_kernel<true><<<dim3(grid), dim3(kT), 0, s>>>(in, in_off, in_bias, n, out, out_off, out_bias, nullptr,
                                                          t.code, t.len, (n + persist - 1) / persist, persist,
                                                          form == 0 ? 1u : 0u);
@@ -1020,6 +1045,8 @@ hipError_t launch_encode(const DevTables &t, const uint8_t *in, const uint64_t *
   // K groups of 64 literals per wave: as many as keep about two waves per
   // SIMD slot (16 per CU) busy
   int K = MHQ_ENC_K ? MHQ_ENC_K : k_env;
+  // (a forced K is rounded down to an instantiated one: 1, 2, 4 or 8)
+  K = K <= 0 ? 0 : K >= 8 ? 8 : K >= 4 ? 4 : K >= 2 ? 2 : 1;
   if (K == 0) {
     const uint64_t slots = (uint64_t)dev::device_cus() * 16u * 2u;
     K = 1;
