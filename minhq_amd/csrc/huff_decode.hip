@@ -353,6 +353,9 @@ __device__ __forceinline__ bool masked_step(const Smem &sm, uint32_t *otgt, BitB
 #ifndef MHQ_DEC_LEAN  // 1: the lean fast loop (LDS pointers, no per-step crossing mask)
 #define MHQ_DEC_LEAN 1
 #endif
+#ifndef MHQ_DEC_UNIFORM  // 1: the lean loop with wave-uniform control flow (branch-free move from A to B)
+#define MHQ_DEC_UNIFORM 0
+#endif
 // The lean form of the fast loop's state: the output word and the next
 // stream word are held as LDS pointers (their addresses need no arithmetic
 // per step), and a step's output word is OR-ed whether or not a code crossed
@@ -426,6 +429,61 @@ __device__ __forceinline__ bool masked_step_lean(const Smem &sm, BitBufL &in, Ou
   out.put(e2 >> 16, (e2 >> 8) & 0xffu);
   in.consume(e2);
   in.refill(w);
+  pend.p = out.op;
+  pend.v = (uint32_t)out.acc;
+  const uint32_t t = out.ab & 32u;
+  out.acc >>= t;
+  out.op += t >> 5;
+  out.ab &= 31u;
+  return stop || in.left < 0;
+}
+
+#ifndef MHQ_DEC_WIN  // 1: the lean loop reads each step's 64-bit window afresh (no refill state)
+#define MHQ_DEC_WIN 0
+#endif
+// A literal's stream with no refill state: each step reads the two staged
+// words holding bit p (one ds_read2) and shifts them to a window of >= 33
+// valid bits, bits past the literal's end forced to ones (so the stop and
+// crossing rules are those of BitBufM).  Fewer instructions per step than the
+// refill; the window read is one more LDS round trip on the step's chain.
+struct WinBuf {
+  uint32_t p;     // bit position in the slice
+  int32_t left;   // endbit - p
+  __device__ __forceinline__ void init(uint32_t p0, uint32_t endbit) {
+    p = p0;
+    left = (int32_t)(endbit - p0);
+  }
+  __device__ __forceinline__ uint64_t window(const uint32_t *words) const {
+    const uint32_t k = p >> 5;
+    const uint64_t w = ((uint64_t)words[k] << 32) | words[k + 1u];
+    // ones from bit `left` (MSB first) on; bit 63 - 63 = bit 0 is never examined
+    const uint32_t c = (uint32_t)min(max(left, 0), 63);
+    return (w << (p & 31u)) | (~0ull >> c);
+  }
+};
+template <bool kLong = true>
+__device__ __forceinline__ bool win_step(const Smem &sm, const uint32_t *words, WinBuf &in, OutAccL &out,
+                                         PendL &pend, bool &stop) {
+  const uint64_t W = in.window(words);
+  const uint32_t S = (uint32_t)(W >> 32);
+  stop = S >= 0xfffffffcu;
+  uint32_t e = sm.lut1[S >> (32 - kLut1Bits)];
+  atomicOr(pend.p, pend.v);
+  bool lng = false;
+  if (kLong && ((e == 0u) & !stop)) {  // a code of 13..29 bits (one branch: no short circuit)
+    uint32_t sym = 0;
+    const uint32_t L = long_code(sm.lut2, S, sym);
+    e = L | (8u << 8) | (sym << 16);
+    lng = true;
+  }
+  out.put(e >> 16, (e >> 8) & 0xffu);
+  const uint64_t W2 = W << (e & 63u);
+  uint32_t e2 = sm.lut1[(uint32_t)(W2 >> 32) >> (32 - kLut1Bits)];
+  e2 = lng ? 0u : e2;
+  out.put(e2 >> 16, (e2 >> 8) & 0xffu);
+  const uint32_t n = (e & 0xffu) + (e2 & 0xffu);
+  in.p += n;
+  in.left -= (int32_t)n;
   pend.p = out.op;
   pend.v = (uint32_t)out.acc;
   const uint32_t t = out.ab & 32u;
@@ -767,7 +825,74 @@ __device__ __forceinline__ void decode_piece(const Smem &sm, WaveSmem &ws, uint3
   const bool roomB = hasB && (B.roomy() || (MHQ_DEC_OPTIMISTIC && B.in_slice()));
   uint32_t rA = kRedo, rB = kRedo;
 #if MHQ_DEC_LEAN
-  bool crossed = false;  // a code crossed a literal's end: the piece is redone (stray output bits)
+#if MHQ_DEC_UNIFORM
+  {
+    // Wave-uniform control flow: the loop runs while any lane has a literal
+    // left, and the move from A to B is branch free.  A lane with nothing
+    // left is frozen on an all-ones window: every step stops at once,
+    // consumes nothing and ORs its last word again (idempotent), and its
+    // result is recomputed unchanged.
+    BitBufL in, inB;  // inB: B's stream, set up once for the in-loop switch
+    in.init(ws.in_w, roomA ? A.p : B.p, roomA ? A.endbit : B.endbit);
+    inB.init(ws.in_w, B.p, B.endbit);
+    OutAccL out, outB;
+    out.init(ws.out_w, roomA ? A.optr : B.optr);
+    outB.init(ws.out_w, B.optr);
+    uint32_t ost = roomA ? ostartA : ostartB;
+    PendL pend{out.op, 0u};
+    bool onB = !roomA, active = roomA || roomB;
+    if (!active) in.bb = ~0ull;
+    while (__ballot(active)) {
+      bool stop;
+#pragma unroll
+      for (int k = 1; k < MHQ_DEC_STEPS; k++) masked_step_lean<MHQ_DEC_LONG1 != 0>(sm, in, out, pend, stop);
+      const bool fin = masked_step_lean(sm, in, out, pend, stop);
+      // stop: the EOS prefix (INVALID when a 31st bit of the literal follows);
+      // left < 0: a code crossed the end (the piece is redone, below)
+      const uint32_t r = in.left < 0 ? kRedo : (out.optr(ws.out_w) - ost) | ((uint32_t)(in.left > kEosOnes) << 31);
+      rA = fin && !onB ? r : rA;
+      rB = fin && onB ? r : rB;
+      const bool sw = fin && !onB && roomB;  // A done: on to B
+      active = active && (!fin || sw);
+      in.bb = sw ? inB.bb : (active ? in.bb : ~0ull);
+      in.left = sw ? inB.left : in.left;
+      in.rem = sw ? inB.rem : in.rem;
+      in.wp = sw ? inB.wp : in.wp;
+      out.acc = sw ? 0ull : out.acc;
+      out.op = sw ? outB.op : out.op;
+      out.ab = sw ? outB.ab : out.ab;
+      ost = sw ? ostartB : ost;
+      onB = onB || sw;
+    }
+    atomicOr(pend.p, pend.v);
+  }
+#elif MHQ_DEC_WIN
+  {
+    WinBuf in;
+    in.init(roomA ? A.p : B.p, roomA ? A.endbit : B.endbit);
+    OutAccL out;
+    out.init(ws.out_w, roomA ? A.optr : B.optr);
+    uint32_t ost = roomA ? ostartA : ostartB;
+    PendL pend{out.op, 0u};
+    bool onB = !roomA, active = roomA || roomB;
+    while (active) {
+      bool stop;
+#pragma unroll
+      for (int k = 1; k < MHQ_DEC_STEPS; k++) win_step<MHQ_DEC_LONG1 != 0>(sm, ws.in_w, in, out, pend, stop);
+      if (win_step(sm, ws.in_w, in, out, pend, stop)) {
+        const uint32_t r = in.left < 0 ? kRedo : (out.optr(ws.out_w) - ost) | ((uint32_t)(in.left > kEosOnes) << 31);
+        rA = onB ? rA : r;
+        rB = onB ? r : rB;
+        active = !onB && roomB;
+        in.init(B.p, B.endbit);
+        out.init(ws.out_w, B.optr);
+        ost = ostartB;
+        onB = true;
+      }
+    }
+    atomicOr(pend.p, pend.v);
+  }
+#else
   {
     BitBufL in, inB;  // inB: B's stream, set up once for the in-loop switch
     in.init(ws.in_w, roomA ? A.p : B.p, roomA ? A.endbit : B.endbit);
@@ -783,10 +908,8 @@ __device__ __forceinline__ void decode_piece(const Smem &sm, WaveSmem &ws, uint3
       for (int k = 1; k < MHQ_DEC_STEPS; k++) masked_step_lean<MHQ_DEC_LONG1 != 0>(sm, in, out, pend, stop);
       if (masked_step_lean(sm, in, out, pend, stop)) {
         // stop: the EOS prefix (INVALID when a 31st bit of the literal follows);
-        // left < 0: a code crossed the end
-        const bool cr = in.left < 0;
-        crossed |= cr;
-        const uint32_t r = cr ? kRedo : (out.optr(ws.out_w) - ost) | ((uint32_t)(in.left > kEosOnes) << 31);
+        // left < 0: a code crossed the end (the piece is redone, below)
+        const uint32_t r = in.left < 0 ? kRedo : (out.optr(ws.out_w) - ost) | ((uint32_t)(in.left > kEosOnes) << 31);
         rA = onB ? rA : r;
         rB = onB ? r : rB;
         active = !onB && roomB;
@@ -798,6 +921,9 @@ __device__ __forceinline__ void decode_piece(const Smem &sm, WaveSmem &ws, uint3
     }
     atomicOr(pend.p, pend.v);
   }
+#endif
+  // a lane that ran a literal through the fast loop and got no result crossed its end
+  const bool crossed = (roomA && rA == kRedo) || (roomB && rB == kRedo);
 #else
   constexpr bool crossed = false;
   {
