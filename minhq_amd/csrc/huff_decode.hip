@@ -439,7 +439,7 @@ __device__ __forceinline__ bool masked_step_lean(const Smem &sm, BitBufL &in, Ou
 }
 
 #ifndef MHQ_DEC_WIN  // 1: the lean loop reads each step's 64-bit window afresh (no refill state)
-#define MHQ_DEC_WIN 0
+#define MHQ_DEC_WIN 1
 #endif
 // A literal's stream with no refill state: each step reads the two staged
 // words holding bit p (one ds_read2) and shifts them to a window of >= 33
@@ -447,24 +447,27 @@ __device__ __forceinline__ bool masked_step_lean(const Smem &sm, BitBufL &in, Ou
 // crossing rules are those of BitBufM).  Fewer instructions per step than the
 // refill; the window read is one more LDS round trip on the step's chain.
 struct WinBuf {
-  uint32_t p;     // bit position in the slice
+  uint32_t pa;    // bit position as an LDS bit address: 8 * (byte address of the staged words) + p
   int32_t left;   // endbit - p
-  __device__ __forceinline__ void init(uint32_t p0, uint32_t endbit) {
-    p = p0;
+  __device__ __forceinline__ void init(const uint32_t *words, uint32_t p0, uint32_t endbit) {
+    pa = 8u * (uint32_t)(uintptr_t)words + p0;
     left = (int32_t)(endbit - p0);
   }
-  __device__ __forceinline__ uint64_t window(const uint32_t *words) const {
-    const uint32_t k = p >> 5;
-    const uint64_t w = ((uint64_t)words[k] << 32) | words[k + 1u];
-    // ones from bit `left` (MSB first) on; bit 63 - 63 = bit 0 is never examined
-    const uint32_t c = (uint32_t)min(max(left, 0), 63);
-    return (w << (p & 31u)) | (~0ull >> c);
+  __device__ __forceinline__ uint64_t window() const {
+    typedef __attribute__((address_space(3))) const uint32_t lds_u32;
+    lds_u32 *w = (lds_u32 *)(uintptr_t)((pa >> 3) & ~3u);
+    const uint64_t x = ((uint64_t)w[0] << 32) | w[1];
+    // ones from bit `left` (MSB first) on, in the high word only: the probes
+    // and the stop test read the top 32 bits, and a second probe's 12 bits
+    // lie in them too (the first consumes at most 12)
+    const uint32_t c = (uint32_t)min(max(left, 0), 32);
+    return (x << (pa & 31u)) | ((uint64_t)(uint32_t)(0xffffffffull >> c) << 32);
   }
 };
 template <bool kLong = true>
 __device__ __forceinline__ bool win_step(const Smem &sm, const uint32_t *words, WinBuf &in, OutAccL &out,
                                          PendL &pend, bool &stop) {
-  const uint64_t W = in.window(words);
+  const uint64_t W = in.window();
   const uint32_t S = (uint32_t)(W >> 32);
   stop = S >= 0xfffffffcu;
   uint32_t e = sm.lut1[S >> (32 - kLut1Bits)];
@@ -482,7 +485,7 @@ __device__ __forceinline__ bool win_step(const Smem &sm, const uint32_t *words, 
   e2 = lng ? 0u : e2;
   out.put(e2 >> 16, (e2 >> 8) & 0xffu);
   const uint32_t n = (e & 0xffu) + (e2 & 0xffu);
-  in.p += n;
+  in.pa += n;
   in.left -= (int32_t)n;
   pend.p = out.op;
   pend.v = (uint32_t)out.acc;
@@ -869,7 +872,7 @@ __device__ __forceinline__ void decode_piece(const Smem &sm, WaveSmem &ws, uint3
 #elif MHQ_DEC_WIN
   {
     WinBuf in;
-    in.init(roomA ? A.p : B.p, roomA ? A.endbit : B.endbit);
+    in.init(ws.in_w, roomA ? A.p : B.p, roomA ? A.endbit : B.endbit);
     OutAccL out;
     out.init(ws.out_w, roomA ? A.optr : B.optr);
     uint32_t ost = roomA ? ostartA : ostartB;
@@ -884,7 +887,7 @@ __device__ __forceinline__ void decode_piece(const Smem &sm, WaveSmem &ws, uint3
         rA = onB ? rA : r;
         rB = onB ? r : rB;
         active = !onB && roomB;
-        in.init(B.p, B.endbit);
+        in.init(ws.in_w, B.p, B.endbit);
         out.init(ws.out_w, B.optr);
         ost = ostartB;
         onB = true;

@@ -10,6 +10,9 @@ times, then runs each disturbance in turn and times the decode again after
 it.  Disturbances:
   devalloc  8 GiB of device memory allocated, touched and freed (torch, then
             empty_cache)
+  devkeep   the same, without empty_cache (torch keeps the memory cached)
+  smallfree 64 MiB of device memory allocated and freed (empty_cache)
+  sleep     2 s idle
   pinalloc  2 GiB of pinned host memory allocated, touched and freed
   bigdec    config 5's host decode (4 x 2^20 x 128 B adversarial literals)
   lenbig    encode_len of the batch with 16 MB chunks (MHQ_HOST_LEN_CHUNK_MB
@@ -33,7 +36,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--steps", default="devalloc,pinalloc,encode,lenbig,bigdec,newctx")
+    ap.add_argument("--steps", default="devalloc,sleep,pinalloc,devkeep,smallfree,encode,lenbig,bigdec,newctx")
     args = ap.parse_args()
     import torch
 
@@ -57,7 +60,23 @@ def main():
         assert not st.any() and np.array_equal(out_len.astype(np.uint64), np.diff(b.off))
         return round(b.nbytes / (t1 - t0) / (1 << 30), 2)
 
-    res = {"first": [dec() for _ in range(4)]}
+    bw_h = torch.empty(256 << 20, dtype=torch.uint8).pin_memory()  # (allocated once: pinning is itself a step)
+    bw_d = torch.empty(256 << 20, dtype=torch.uint8, device="cuda")
+
+    def rawbw():  # pinned host -> device and back, 256 MiB, torch copies
+        h, d = bw_h, bw_d
+        d.copy_(h, non_blocking=True)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        d.copy_(h, non_blocking=True)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        h.copy_(d, non_blocking=True)
+        torch.cuda.synchronize()
+        t2 = time.perf_counter()
+        return {"h2d": round(0.25 / (t1 - t0), 2), "d2h": round(0.25 / (t2 - t1), 2)}
+
+    res = {"first": [dec() for _ in range(4)], "rawbw_first": rawbw()}
     for step in args.steps.split(","):
         t0 = time.perf_counter()
         if step == "devalloc":
@@ -66,6 +85,18 @@ def main():
             torch.cuda.synchronize()
             del x
             torch.cuda.empty_cache()
+        elif step == "devkeep":
+            x = torch.empty(8 << 30, dtype=torch.uint8, device="cuda")
+            x.fill_(1)
+            torch.cuda.synchronize()
+            del x
+        elif step == "smallfree":
+            x = torch.empty(64 << 20, dtype=torch.uint8, device="cuda")
+            torch.cuda.synchronize()
+            del x
+            torch.cuda.empty_cache()
+        elif step == "sleep":
+            time.sleep(2)
         elif step == "pinalloc":
             x = torch.empty(2 << 30, dtype=torch.uint8).pin_memory()
             x.fill_(1)
@@ -86,7 +117,7 @@ def main():
         else:
             raise SystemExit(f"unknown step {step}")
         took = round(time.perf_counter() - t0, 2)
-        res[step] = {"after": [dec() for _ in range(3)], "step_s": took}
+        res[step] = {"after": [dec() for _ in range(3)], "step_s": took, "rawbw": rawbw()}
         print(step, res[step], file=sys.stderr, flush=True)
     res["env"] = {k: os.environ.get(k) for k in ("MHQ_HOST_CHUNK_MB", "MHQ_HOST_LEN_CHUNK_MB")}
     print(json.dumps(res), flush=True)
