@@ -177,9 +177,52 @@ __device__ void encode_literal_global(const uint8_t *src, uint64_t nbytes, uint8
 }
 
 // Encodes staged plaintext bytes [p, e); returns the encoded bit count.
-// Per staged word: its four code lookups are issued together (bytes outside
-// [p, e) look up harmlessly and contribute nothing) and the next word is read
-// ahead, so a word costs one LDS round trip, not one per byte.
+// Per staged word: its four code lookups are issued together and the next
+// word is read ahead, so a word costs one LDS round trip, not one per byte.
+// Only the literal's first and last words hold bytes outside [p, e) (they
+// look up harmlessly and are masked to nothing); the words between them are
+// put without the per-byte range tests (MHQ_ENC_MIDLOOP).
+#ifndef MHQ_ENC_MIDLOOP
+#define MHQ_ENC_MIDLOOP 1
+#endif
+template <bool kEmit, bool kMasked>
+__device__ __forceinline__ void encode_word(const Smem<kEmit> &sm, uint32_t w, uint32_t q, uint32_t p, uint32_t e,
+                                            BitOut &bo, uint32_t &bits) {
+  uint2 c[4];
+#pragma unroll
+  for (int b = 0; b < 4; b++) c[b] = sm.code[(w >> (8 * b)) & 0xffu];
+  uint32_t len[4], code[4];
+#pragma unroll
+  for (int b = 0; b < 4; b++) {
+    const uint32_t x = q + (uint32_t)b;
+    const bool in = !kMasked || (x >= p && x < e);
+    len[b] = in ? c[b].y : 0u;
+    code[b] = in ? c[b].x : 0u;
+  }
+  const uint32_t l4 = len[0] + len[1] + len[2] + len[3];
+  bits += l4;
+#if MHQ_ENC_QUAD
+  // The word's four codes as one put when they fit 32 bits (text: nearly
+  // always): one LDS OR per word instead of one per byte.
+  if (kEmit) {
+    if (l4 <= 32u) {
+      uint32_t cc = code[0];
+#pragma unroll
+      for (int b = 1; b < 4; b++) cc = (cc << len[b]) | code[b];
+      bo.put(cc, l4);
+    } else {
+#pragma unroll
+      for (int b = 0; b < 4; b++) bo.put(code[b], len[b]);
+    }
+  }
+#else
+  if (kEmit) {
+#pragma unroll
+    for (int b = 0; b < 4; b++) bo.put(code[b], len[b]);
+  }
+#endif
+}
+
 template <bool kEmit>
 __device__ __forceinline__ uint32_t encode_one(Smem<kEmit> &sm, uint32_t p, uint32_t e, uint32_t ostart) {
   uint32_t bits = 0;
@@ -187,43 +230,27 @@ __device__ __forceinline__ uint32_t encode_one(Smem<kEmit> &sm, uint32_t p, uint
   if (kEmit) bo.init(sm.out_w, ostart);
   uint32_t q = p & ~3u;
   uint32_t w = sm.in_w[q >> 2];
+#if MHQ_ENC_MIDLOOP
+  if (q < e) {
+    // the first word (bytes before p), then whole words, then the last partial word
+    uint32_t wn = sm.in_w[(q >> 2) + 1u];  // in_w has slack words past the slice
+    encode_word<kEmit, true>(sm, w, q, p, e, bo, bits);
+    w = wn;
+    q += 4u;
+    for (; q + 4u <= e; q += 4u) {
+      wn = sm.in_w[(q >> 2) + 1u];
+      encode_word<kEmit, false>(sm, w, q, p, e, bo, bits);
+      w = wn;
+    }
+    if (q < e) encode_word<kEmit, true>(sm, w, q, p, e, bo, bits);
+  }
+#else
   for (; q < e; q += 4u) {
     const uint32_t wn = sm.in_w[(q >> 2) + 1u];  // in_w has slack words past the slice
-    uint2 c[4];
-#pragma unroll
-    for (int b = 0; b < 4; b++) c[b] = sm.code[(w >> (8 * b)) & 0xffu];
-    uint32_t len[4], code[4];
-#pragma unroll
-    for (int b = 0; b < 4; b++) {
-      const uint32_t x = q + (uint32_t)b;
-      const bool in = x >= p && x < e;
-      len[b] = in ? c[b].y : 0u;
-      code[b] = in ? c[b].x : 0u;
-    }
-    const uint32_t l4 = len[0] + len[1] + len[2] + len[3];
-    bits += l4;
-#if MHQ_ENC_QUAD
-    // The word's four codes as one put when they fit 32 bits (text: nearly
-    // always): one LDS OR per word instead of one per byte.
-    if (kEmit) {
-      if (l4 <= 32u) {
-        uint32_t cc = code[0];
-#pragma unroll
-        for (int b = 1; b < 4; b++) cc = (cc << len[b]) | code[b];
-        bo.put(cc, l4);
-      } else {
-#pragma unroll
-        for (int b = 0; b < 4; b++) bo.put(code[b], len[b]);
-      }
-    }
-#else
-    if (kEmit) {
-#pragma unroll
-      for (int b = 0; b < 4; b++) bo.put(code[b], len[b]);
-    }
-#endif
+    encode_word<kEmit, true>(sm, w, q, p, e, bo, bits);
     w = wn;
   }
+#endif
   if (kEmit) bo.finish();
   return bits;
 }
