@@ -332,7 +332,9 @@ int run_chunk(Device *d, Stage &S, const HostJob &j, uint64_t a, uint64_t b) {
   // few MB per chunk).  Encode needs none: both encode kernels write every
   // byte of a region (host-path regions are exactly enc_len long).
   uint8_t *dout = (uint8_t *)S.out.p;
+#ifndef MHQ_X_NOMEMSET  // (host-path experiment only: bytes past out_len left as they were)
   if (j.op == Op::kDecode) MHQ_TRY(hipMemsetAsync(dout, 0, out_bytes, s));
+#endif
   const uint64_t *dout_off = (const uint64_t *)S.out_off.p;
   if (j.op == Op::kEncode) {
     MHQ_TRY(mhq::launch_encode(d->tables, din, din_off, in_bias, m, dout, dout_off, out_bias, s));
