@@ -464,40 +464,6 @@ struct WinBuf {
     return (x << (pa & 31u)) | ((uint64_t)(uint32_t)(0xffffffffull >> c) << 32);
   }
 };
-// MHQ_DEC_WIN 2: the window's words come from a read issued one step earlier:
-// a step reads words k..k+2 at its own word k = p/32, and the next step's
-// window (p' <= p + 30: word k or k+1 and the one after) is in them, so the
-// read is off the step's chain (two LDS instructions instead of one).
-struct WinBuf2 {
-  uint32_t pa;     // LDS bit address of the next bit
-  int32_t left;    // endbit - p
-  uint32_t w0, w1, w2;  // staged words k0, k0 + 1, k0 + 2 (k0 = the previous step's word)
-  uint32_t r0;     // the previous step's pa & 31
-  __device__ __forceinline__ void fetch() {
-    typedef __attribute__((address_space(3))) const uint32_t lds_u32;
-    lds_u32 *w = (lds_u32 *)(uintptr_t)((pa >> 3) & ~3u);
-    w0 = w[0];
-    w1 = w[1];
-    w2 = w[2];
-    r0 = pa & 31u;
-  }
-  __device__ __forceinline__ void init(const uint32_t *words, uint32_t p0, uint32_t endbit) {
-    pa = 8u * (uint32_t)(uintptr_t)words + p0;
-    left = (int32_t)(endbit - p0);
-    fetch();
-  }
-  // this step's window (its words are the last fetch's), then the next fetch
-  __device__ __forceinline__ uint64_t window() {
-    const uint32_t r = pa & 31u;
-    const bool adv = r < r0;  // p moved into the next word (a step consumes at most 30 bits)
-    const uint32_t hi = adv ? w1 : w0, lo = adv ? w2 : w1;
-    const uint64_t x = ((uint64_t)hi << 32) | lo;
-    const uint32_t c = (uint32_t)min(max(left, 0), 32);
-    fetch();
-    return (x << r) | ((uint64_t)(uint32_t)(0xffffffffull >> c) << 32);
-  }
-};
-
 template <bool kLong = true, class WB>
 __device__ __forceinline__ bool win_step(const Smem &sm, const uint32_t *words, WB &in, OutAccL &out,
                                          PendL &pend, bool &stop) {
@@ -905,11 +871,7 @@ __device__ __forceinline__ void decode_piece(const Smem &sm, WaveSmem &ws, uint3
   }
 #elif MHQ_DEC_WIN
   {
-#if MHQ_DEC_WIN == 2
-    WinBuf2 in;
-#else
     WinBuf in;
-#endif
     in.init(ws.in_w, roomA ? A.p : B.p, roomA ? A.endbit : B.endbit);
     OutAccL out;
     out.init(ws.out_w, roomA ? A.optr : B.optr);

@@ -14,6 +14,8 @@
 #include <string.h>
 
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
 #include <memory>
 #include <mutex>
 #include <thread>
@@ -348,14 +350,87 @@ int run_chunk(Device *d, Stage &S, const HostJob &j, uint64_t a, uint64_t b) {
       hipMemcpyAsync(j.out + (j.out_off[a] - j.out_off[0]), dout, out_bytes, hipMemcpyDeviceToHost, s));
 }
 
-// Runs literals [a, b) of a host-memory job on one device: chunks of about
-// kChunkBytes of input (kLenChunkBytes for encode_len), pipelined over the
-// device's kPipe stages.
+#ifndef MHQ_HOST_ZERO_COPY  // 0: host-memory calls always stage through device buffers
+#define MHQ_HOST_ZERO_COPY 1
+#endif
+// Bytes past an input buffer's end that must lie in its mapping before a
+// kernel reads it in place: the kernels read aligned 16-B chunks holding a
+// valid byte (never a chunk wholly past the end), so 16 would do; 64 is
+// margin.  Outputs need none: the kernels write exactly their regions.
+constexpr uint64_t kZcSlack = 64;
+
+// The device's view of host memory [p, p + len) when it lies in one pinned
+// allocation the device maps (hipHostMalloc, torch's pin_memory) with
+// `slack` bytes after it, else null (pageable memory, hipHostRegister'ed
+// ranges whose extent the runtime does not report, buffers at a mapping's
+// very end: those go through the staged copies).
+const void *zero_copy_view(const void *p, uint64_t len, uint64_t slack = kZcSlack) {
+  if (!p) return nullptr;
+  hipPointerAttribute_t at{};
+  if (hipPointerGetAttributes(&at, p) != hipSuccess || at.type != hipMemoryTypeHost || !at.devicePointer) {
+    (void)hipGetLastError();  // (pageable memory reports an error: not the caller's)
+    return nullptr;
+  }
+  hipDeviceptr_t base = nullptr;
+  size_t size = 0;
+  if (hipMemGetAddressRange(&base, &size, (hipDeviceptr_t)p) != hipSuccess || !base) {
+    (void)hipGetLastError();
+    return nullptr;
+  }
+  const uintptr_t b0 = (uintptr_t)base, x = (uintptr_t)p;
+  if (b0 % 4096u) return nullptr;
+  const uint64_t mapped = ((uint64_t)size + 4095u) & ~(uint64_t)4095u;  // pinned pages are mapped whole
+  if (x < b0 || x - b0 + len + slack > mapped) return nullptr;
+  return at.devicePointer;
+}
+
+// A host-memory job run in place: every buffer the op touches is pinned and
+// mapped, so the kernels read and write it over PCIe with no staging copies
+// (one launch per device shard).  Returns false (nothing enqueued) otherwise.
+bool run_zero_copy(Device *d, const HostJob &j, uint64_t a, uint64_t b, int &rc) {
+  if (!MHQ_HOST_ZERO_COPY) return false;
+  const uint64_t m = b - a;
+  const uint64_t n_all_in = j.in_off[b] - j.in_off[0];  // the view must reach the shard's end
+  const uint8_t *din = (const uint8_t *)zero_copy_view(j.in, n_all_in ? n_all_in : 1);
+  const uint64_t *din_off = (const uint64_t *)zero_copy_view(j.in_off + a, (m + 1) * sizeof(uint64_t));
+  if (!din || !din_off) return false;
+  hipStream_t s = d->st[0].s;
+  if (j.op == Op::kEncodeLen) {
+    uint32_t *dl = (uint32_t *)zero_copy_view(j.lens + a, m * sizeof(uint32_t), 0);
+    if (!dl) return false;
+    rc = hip_rc(mhq::launch_encode_len(d->tables, din, din_off, j.in_off[0], m, dl, s));
+  } else {
+    const uint64_t n_all_out = j.out_off[b] - j.out_off[0];
+    uint8_t *dout = (uint8_t *)zero_copy_view(j.out, n_all_out ? n_all_out : 1, 0);
+    const uint64_t *dout_off = (const uint64_t *)zero_copy_view(j.out_off + a, (m + 1) * sizeof(uint64_t));
+    if (!dout || !dout_off) return false;
+    if (j.op == Op::kEncode) {
+      rc = hip_rc(mhq::launch_encode(d->tables, din, din_off, j.in_off[0], m, dout, dout_off, j.out_off[0], s));
+    } else {
+      uint32_t *dl = (uint32_t *)zero_copy_view(j.lens + a, m * sizeof(uint32_t), 0);
+      uint8_t *dst = (uint8_t *)zero_copy_view(j.status + a, m, 0);
+      if (!dl || !dst) return false;
+      rc = hip_rc(mhq::launch_decode(d->tables, din, din_off, j.in_off[0], m, dout, dout_off, j.out_off[0], dl, dst,
+                                     s));
+    }
+  }
+  const int r = hip_rc(hipStreamSynchronize(s));
+  if (rc == MHQ_OK) rc = r;
+  return true;
+}
+
+// Runs literals [a, b) of a host-memory job on one device: in place when the
+// buffers allow (run_zero_copy), else in chunks of about kChunkBytes of input
+// (kLenChunkBytes for encode_len), pipelined over the device's kPipe stages.
 int run_shard(Device *d, const HostJob &j, uint64_t a, uint64_t b) {
   const uint64_t m = b - a;
   if (m == 0) return MHQ_OK;
   std::lock_guard<std::mutex> lock(d->mu);
   MHQ_TRY(hipSetDevice(d->ordinal));
+  {
+    int zrc = MHQ_OK;
+    if (run_zero_copy(d, j, a, b, zrc)) return zrc;
+  }
   const uint64_t in_bytes = j.in_off[b] - j.in_off[a];
   const uint64_t chunk = j.op == Op::kEncodeLen ? kLenChunkBytes : kChunkBytes;
   const size_t nch = (size_t)std::max<uint64_t>(1, std::min<uint64_t>(m, (in_bytes + chunk - 1) / chunk));
@@ -381,11 +456,28 @@ int run_shard(Device *d, const HostJob &j, uint64_t a, uint64_t b) {
     }
   }
   int rc = MHQ_OK;
+#ifdef MHQ_X_HOSTPROF  // (host-path experiment: enqueue and wait times per call, on stderr)
+  const auto t0 = std::chrono::steady_clock::now();
+  double worst = 0;
+  for (size_t c = 0; c < nch && rc == MHQ_OK; c++) {
+    const auto c0 = std::chrono::steady_clock::now();
+    rc = run_chunk(d, d->st[c % kPipe], j, a + cb[c], a + cb[c + 1]);
+    worst = std::max(worst, std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - c0).count());
+  }
+  const auto t1 = std::chrono::steady_clock::now();
+#else
   for (size_t c = 0; c < nch && rc == MHQ_OK; c++) rc = run_chunk(d, d->st[c % kPipe], j, a + cb[c], a + cb[c + 1]);
+#endif
   for (int k = 0; k < used; k++) {
     const int r = hip_rc(hipStreamSynchronize(d->st[k].s));
     if (rc == MHQ_OK) rc = r;
   }
+#ifdef MHQ_X_HOSTPROF
+  const auto t2 = std::chrono::steady_clock::now();
+  fprintf(stderr, "hostprof op=%d chunks=%zu enqueue_us=%.0f worst_chunk_us=%.0f wait_us=%.0f\n", (int)j.op, nch,
+          std::chrono::duration<double, std::micro>(t1 - t0).count(), worst,
+          std::chrono::duration<double, std::micro>(t2 - t1).count());
+#endif
   return rc;
 }
 

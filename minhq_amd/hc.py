@@ -144,9 +144,10 @@ class Codec:
     def encode(self, data: np.ndarray, off: np.ndarray, alloc=None) -> Tuple[np.ndarray, np.ndarray]:
         """Returns (encoded bytes, encoded offsets) for a packed batch."""
         n = len(off) - 1
-        # enc_len is read back by the host scan: pageable memory (pinned host
-        # memory can be slow to read from the CPU); the offsets are only written.
-        enc_len = self.encode_len(data, off)
+        # enc_len from the caller's allocator too: in pinned memory the kernel
+        # writes it in place (the host scan reads pinned memory as fast as
+        # pageable: 0.34 vs 0.36 ms for 2^20 lengths, tools/hostpath.py)
+        enc_len = self.encode_len(data, off, alloc=alloc)
         enc_off = _alloc(alloc, n + 1, np.uint64)
         enc_off[0] = 0
         if n:

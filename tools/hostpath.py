@@ -19,6 +19,8 @@ it.  Disturbances:
             is read once per process: run with it set in the environment)
   encode    the host encode (encode_len + host scan + encode) of the batch
   newctx    a second context opened, used and closed
+  repin     (not a disturbance) the inputs and the output pool pinned afresh
+  pageable  (not a disturbance) one decode into pageable outputs
 Prints one JSON line: GiB/s per measurement, in order.
 """
 from __future__ import annotations
@@ -52,10 +54,12 @@ def main():
     enc, eoff = pin(np.array(enc)), pin(np.array(eoff))
     cap = pin(hc.capacity_offsets(eoff))
 
+    S = {"enc": enc, "eoff": eoff, "cap": cap, "dpool": dpool}  # (replaced by the repin step)
+
     def dec():
-        dpool.rewind()
+        S["dpool"].rewind()
         t0 = time.perf_counter()
-        _, _, out_len, st = codec.decode(enc, eoff, cap, alloc=dpool)
+        _, _, out_len, st = codec.decode(S["enc"], S["eoff"], S["cap"], alloc=S["dpool"])
         t1 = time.perf_counter()
         assert not st.any() and np.array_equal(out_len.astype(np.uint64), np.diff(b.off))
         return round(b.nbytes / (t1 - t0) / (1 << 30), 2)
@@ -77,6 +81,23 @@ def main():
         return {"h2d": round(0.25 / (t1 - t0), 2), "d2h": round(0.25 / (t2 - t1), 2)}
 
     res = {"first": [dec() for _ in range(4)], "rawbw_first": rawbw()}
+    # the host scan over encode_len's output: pinned vs pageable (hc.encode)
+    lens_pg = codec.encode_len(data, off)
+    lens_pin = pin(lens_pg.copy())
+    for name, arr in (("pageable", lens_pg), ("pinned", lens_pin)):
+        t0 = time.perf_counter()
+        for _ in range(5):
+            np.cumsum(arr, dtype=np.uint64)
+        res[f"cumsum_{name}_ms"] = round((time.perf_counter() - t0) / 5 * 1e3, 3)
+    epool2 = bench.PinnedPool()
+    for name, al in (("encode_len_pageable", None), ("encode_len_pinned", epool2)):
+        ts = []
+        for _ in range(3):
+            epool2.rewind()
+            t0 = time.perf_counter()
+            codec.encode_len(data, off, alloc=al) if al is not None else codec.encode_len(data, off)
+            ts.append(round(b.nbytes / (time.perf_counter() - t0) / (1 << 30), 2))
+        res[name + "_gib_s"] = ts
     for step in args.steps.split(","):
         t0 = time.perf_counter()
         if step == "devalloc":
@@ -95,6 +116,12 @@ def main():
             torch.cuda.synchronize()
             del x
             torch.cuda.empty_cache()
+        elif step == "pageable":  # (not a disturbance: the decode rate into pageable outputs, for comparison)
+            t0p = time.perf_counter()
+            codec.decode(np.array(enc), np.array(eoff), np.array(cap))
+            res["pageable_gib_s"] = round(b.nbytes / (time.perf_counter() - t0p) / (1 << 30), 2)
+        elif step == "repin":  # inputs and output pool pinned afresh
+            S.update(dpool=bench.PinnedPool(), enc=pin(np.array(enc)), eoff=pin(np.array(eoff)), cap=pin(np.array(cap)))
         elif step == "sleep":
             time.sleep(2)
         elif step == "pinalloc":
@@ -117,7 +144,8 @@ def main():
         else:
             raise SystemExit(f"unknown step {step}")
         took = round(time.perf_counter() - t0, 2)
-        res[step] = {"after": [dec() for _ in range(3)], "step_s": took, "rawbw": rawbw()}
+        res[step] = {"after": [dec() for _ in range(int(os.environ.get("HOSTPATH_AFTER", "3")))], "step_s": took,
+                     "rawbw": rawbw()}
         print(step, res[step], file=sys.stderr, flush=True)
     res["env"] = {k: os.environ.get(k) for k in ("MHQ_HOST_CHUNK_MB", "MHQ_HOST_LEN_CHUNK_MB")}
     print(json.dumps(res), flush=True)
