@@ -632,7 +632,7 @@ typedef __attribute__((address_space(1))) const void g_void;
 struct TileOff {  // raw loads: in_off / out_off of literals s + 2*lane + {0, 1}, and of s + tile
   uint64_t i0, o0, ie, oe;
   uint32_t i1, o1;  // only their low words are used (tile-relative offsets): 32-bit loads
-  uint32_t e0, e1;  // kGaps: in_end of the two literals (low words)
+  uint32_t e0, e1;  // kGaps: in_end of the two literals (low words: in_end is a u32 array of them)
 };
 // The low word of a u64 offset.
 __device__ __forceinline__ uint32_t lo32(const uint64_t *a, uint64_t j) { return ((const uint32_t *)a)[2u * j]; }
@@ -654,7 +654,7 @@ __device__ __forceinline__ uint64_t uniform64(uint64_t v) {
 // tile past the range loads the range end).
 template <bool kGaps>
 __device__ __forceinline__ void load_off(TileOff &t, const uint64_t *__restrict__ in_off,
-                                         const uint64_t *__restrict__ in_end, const uint64_t *__restrict__ out_off,
+                                         const uint32_t *__restrict__ in_end, const uint64_t *__restrict__ out_off,
                                          uint64_t s, uint64_t L1, uint32_t tl, uint32_t lane) {
   const uint32_t z = vzero();  // keeps the loads per-lane vector loads
   const uint64_t j0 = min(s + 2u * lane, L1) + z, j1 = min(s + 2u * lane + 1u, L1) + z;
@@ -662,8 +662,8 @@ __device__ __forceinline__ void load_off(TileOff &t, const uint64_t *__restrict_
   t.i0 = in_off[j0];
   t.i1 = lo32(in_off, j1);
   if (kGaps) {  // (in_end has n entries: indices clamped below L1)
-    t.e0 = lo32(in_end, min(j0, L1 - 1u));
-    t.e1 = lo32(in_end, min(j1, L1 - 1u));
+    t.e0 = in_end[min(j0, L1 - 1u)];
+    t.e1 = in_end[min(j1, L1 - 1u)];
   }
   t.o0 = out_off[j0];
   t.o1 = lo32(out_off, j1);
@@ -674,7 +674,7 @@ __device__ __forceinline__ void load_off(TileOff &t, const uint64_t *__restrict_
 // The two halves of load_off, for the launch's opening.
 template <bool kGaps>
 __device__ __forceinline__ void load_off_in(TileOff &t, const uint64_t *__restrict__ in_off,
-                                            const uint64_t *__restrict__ in_end, uint64_t s, uint64_t L1,
+                                            const uint32_t *__restrict__ in_end, uint64_t s, uint64_t L1,
                                             uint32_t tl, uint32_t lane) {
   const uint32_t z = vzero();
   const uint64_t j0 = min(s + 2u * lane, L1) + z, j1 = min(s + 2u * lane + 1u, L1) + z;
@@ -682,8 +682,8 @@ __device__ __forceinline__ void load_off_in(TileOff &t, const uint64_t *__restri
   t.i0 = in_off[j0];
   t.i1 = lo32(in_off, j1);
   if (kGaps) {
-    t.e0 = lo32(in_end, min(j0, L1 - 1u));
-    t.e1 = lo32(in_end, min(j1, L1 - 1u));
+    t.e0 = in_end[min(j0, L1 - 1u)];
+    t.e1 = in_end[min(j1, L1 - 1u)];
   }
   t.ie = in_off[je];
 }
@@ -734,25 +734,60 @@ __device__ __forceinline__ void put_chunk(WaveSmem &ws, uint32_t c, u32x4 v) {
   *(u32x4 *)(ws.in_w + 4u * c) = v;
 }
 
+// read_strings' outcome of a decoded string (hc/io.go:92-96), applied where
+// the decode writes it when `str_kind` (the framed strings' kinds) is given:
+// INVALID keeps length 0; a Huffman string that decoded to nothing is io.EOF.
+// (Raw and unreadable strings are empty literals here: 0 / OK, as the
+// reference returns for the unreadable ones; raw payloads are the finish
+// pass's.)
+constexpr uint32_t kStrEof = 2;  // MHQ_STR_EOF (include/mhq_huff.h)
+__device__ __forceinline__ void str_outcome(const uint8_t *__restrict__ str_kind, uint64_t i, uint32_t &len,
+                                            uint32_t &st) {
+  if (st != 0u)
+    len = 0;
+  else if (len == 0u && (str_kind[i] & 3u) == 1u)
+    st = kStrEof;
+}
+
 // out_len / status of literals [s, s + m) from the wave's len array.
 __device__ __forceinline__ void flush_lens(const WaveSmem &ws, uint64_t s, uint32_t m, uint32_t *__restrict__ out_len,
-                                           uint8_t *__restrict__ status, uint32_t lane) {
+                                           uint8_t *__restrict__ status, uint32_t lane,
+                                           const uint8_t *__restrict__ str_kind = nullptr) {
 #pragma unroll
   for (int h = 0; h < 2; h++) {
     const uint32_t j = lane + (uint32_t)kWave * h;
     if (j < m) {
       const uint32_t v = ws.len[j];
-      out_len[s + j] = v & 0x7fffffffu;
-      status[s + j] = (uint8_t)(v >> 31);
+      uint32_t len = v & 0x7fffffffu, st = v >> 31;
+      if (str_kind) str_outcome(str_kind, s + j, len, st);
+      out_len[s + j] = len;
+      status[s + j] = (uint8_t)st;
     }
   }
 }
 
 // Decodes the m literals whose boundary records rec[0..m] and input bytes are
 // staged: zero the output region, sort, decode into out_w / len.
+#ifndef MHQ_DEC_LOOPPRIO  // probe-loop priority by the wave's tile count (0: all loops at priority 0)
+#define MHQ_DEC_LOOPPRIO 2
+#endif
+// A wave's loop priority: with every loop at one priority the SIMD issues
+// oldest-first, so a SIMD's three waves finish their equal work one after the
+// other and the last runs alone (the age staircase).  Loops of
+// earlier tiles at a higher priority let the younger waves catch up at every
+// tile boundary.
+[[maybe_unused]] __device__ __forceinline__ void set_loop_prio(uint32_t p) {
+  if (p >= 2u)
+    __builtin_amdgcn_s_setprio(2);
+  else if (p == 1u)
+    __builtin_amdgcn_s_setprio(1);
+  else
+    __builtin_amdgcn_s_setprio(0);
+}
+
 template <bool kGaps>
 __device__ __forceinline__ void decode_piece(const Smem &sm, WaveSmem &ws, uint32_t m, uint32_t out_bytes,
-                                             uint32_t lane, [[maybe_unused]] int tls = -1) {
+                                             uint32_t lane, [[maybe_unused]] int tls = -1, uint32_t prio = 0) {
   for (uint32_t c = lane; c < (out_bytes + 15u) >> 4; c += kWave) *(u32x4 *)(ws.out_w + 4u * c) = u32x4{0u, 0u, 0u, 0u};
 #ifdef MHQ_X_DBLZERO  // timing experiment: the zeroing twice
   wave_sync();
@@ -813,7 +848,9 @@ __device__ __forceinline__ void decode_piece(const Smem &sm, WaveSmem &ws, uint3
   B.load(ws, hasB ? ws.order[2u * kWave - 1u - lane] : 0u);
   const uint32_t ostartA = A.optr, ostartB = B.optr;
   TL(tls);
-#if MHQ_DEC_PRIO
+#if MHQ_DEC_LOOPPRIO
+  set_loop_prio(prio);
+#elif MHQ_DEC_PRIO
   __builtin_amdgcn_s_setprio(0);  // the probe loop at normal priority
 #endif
   // Every literal runs the masked loop to its end (ones past the end: no end
@@ -1169,11 +1206,11 @@ __device__ __forceinline__ void long_step(const Smem &sm, uint32_t *otgt, BB &in
 
 template <bool kGaps>
 __device__ void decode_tile_long(const Smem &sm, WaveSmem &ws, const uint8_t *__restrict__ in,
-                                 const uint64_t *__restrict__ in_off, const uint64_t *__restrict__ in_end,
+                                 const uint64_t *__restrict__ in_off, const uint32_t *__restrict__ in_end,
                                  uint64_t in_bias, uint8_t *__restrict__ out,
                                  const uint64_t *__restrict__ out_off, uint64_t out_bias,
                                  uint32_t *__restrict__ out_len, uint8_t *__restrict__ status, uint64_t s,
-                                 uint32_t cnt, uint32_t lane) {
+                                 uint32_t cnt, uint32_t lane, const uint8_t *__restrict__ str_kind = nullptr) {
   uint32_t *win = ws.in_w + lane * kLongWords;  // spans the input and output slices
   const uint32_t swz = (lane & 7u) << 2;         // BitBufS: the window's chunk swizzle
   constexpr uint32_t kWinBits = kLongWords * 32u;
@@ -1191,13 +1228,21 @@ __device__ void decode_tile_long(const Smem &sm, WaveSmem &ws, const uint8_t *__
     have = false;
     while (j < cnt) {
       ib = in_off[s + j];
-      ie = kGaps ? in_end[s + j] : in_off[s + j + 1];
+      if (kGaps) {  // the end's low word: the end is the first at or after ib with it
+        const uint32_t e = in_end[s + j];
+        ie = (ib & ~0xffffffffull) | e;
+        if (e < (uint32_t)ib) ie += 1ull << 32;
+      } else {
+        ie = in_off[s + j + 1];
+      }
       ob = out_off[s + j];
       const uint64_t oe = out_off[s + j + 1];
       uint8_t *o = out + (ob - out_bias);
       if (ie == ib) {  // nothing to read: Read at EOF
-        out_len[s + j] = 0;
-        status[s + j] = 0;
+        uint32_t len = 0, st = 0;
+        if (kGaps && str_kind) str_outcome(str_kind, s + j, len, st);
+        out_len[s + j] = len;
+        status[s + j] = (uint8_t)st;
       } else if (oe - ob < (ie - ib) * 8u / 5u) {  // a truncating region: the exact slow path
         decode_literal_global(in + (ib - in_bias), ie - ib, o, oe - ob, sm, out_len + s + j, status + s + j);
       } else {
@@ -1274,10 +1319,11 @@ __device__ void decode_tile_long(const Smem &sm, WaveSmem &ws, const uint8_t *__
       const bool stopped = lim == -1 && lim0 != -1;  // a fast step finished the literal (EOS prefix, long code past the end)
       if (stopped || ends_here) {
         const uint32_t st = stopped ? bad : end_checked_g<BitBufS>(sm, win, bin.p, endw, acc, gout, swz);
-        const uint32_t got = acc.optr() - ostart;
+        uint32_t got = acc.optr() - ostart, st2 = st;
         acc.finish(gout);
+        if (kGaps && str_kind) str_outcome(str_kind, s + j, got, st2);
         out_len[s + j] = got;
-        status[s + j] = (uint8_t)st;
+        status[s + j] = (uint8_t)st2;
         j += kWave;
         next_lit();
       } else {
@@ -1348,7 +1394,8 @@ __device__ void decode_tile_pieces(const Smem &sm, WaveSmem &ws, const uint8_t *
 // its len slot until the results overwrite it.
 template <bool kGaps>
 __global__ __launch_bounds__(kT) void decode_kernel(const uint8_t *__restrict__ in, const uint64_t *__restrict__ in_off,
-                                                    const uint64_t *__restrict__ in_end,
+                                                    const uint32_t *__restrict__ in_end,
+                                                    const uint8_t *__restrict__ str_kind,
                                                     uint64_t in_bias, uint64_t n, uint8_t *__restrict__ out,
                                                     const uint64_t *__restrict__ out_off, uint64_t out_bias,
                                                     uint32_t *__restrict__ out_len, uint8_t *__restrict__ status,
@@ -1500,7 +1547,7 @@ __global__ __launch_bounds__(kT) void decode_kernel(const uint8_t *__restrict__ 
       wave_sync();
       store_out(pd_o, (const uint8_t *)ws.out_w, pd_lo, pd_hi, lane);
 #endif
-      flush_lens(ws, pd_s, pd_m, out_len, status, lane);
+      flush_lens(ws, pd_s, pd_m, out_len, status, lane, kGaps ? str_kind : nullptr);
     }
     pd_o = nullptr;
     wave_sync();
@@ -1513,7 +1560,11 @@ __global__ __launch_bounds__(kT) void decode_kernel(const uint8_t *__restrict__ 
         wave_sync();
       }
       const uint32_t out_bytes = ws.rec[cnt] >> 16;
-      decode_piece<kGaps>(sm, ws, cnt, out_bytes, lane, tl_slot(tl_j, 3));
+#if MHQ_DEC_LOOPPRIO == 2
+      decode_piece<kGaps>(sm, ws, cnt, out_bytes, lane, tl_slot(tl_j, 3), tl_j < 2u ? 1u : 0u);
+#else
+      decode_piece<kGaps>(sm, ws, cnt, out_bytes, lane, tl_slot(tl_j, 3), tl_j < 2u ? 2u - tl_j : 0u);
+#endif
       pd_o = oa - odelta;
       pd_lo = odelta;
       pd_hi = out_bytes;
@@ -1531,7 +1582,7 @@ __global__ __launch_bounds__(kT) void decode_kernel(const uint8_t *__restrict__ 
         decode_tile_pieces(sm, ws, in, in_off, in_bias, out, out_off, out_bias, out_len, status, s, cnt, lane);
       else
         decode_tile_long<kGaps>(sm, ws, in, in_off, in_end, in_bias, out, out_off, out_bias, out_len, status, s,
-                                cnt, lane);
+                                cnt, lane, kGaps ? str_kind : nullptr);
     }
     TL(tl_slot(tl_j, 5));
     tl_j++;
@@ -1541,7 +1592,7 @@ __global__ __launch_bounds__(kT) void decode_kernel(const uint8_t *__restrict__ 
   }
   if (pd_o) {
     store_out(pd_o, (const uint8_t *)ws.out_w, pd_lo, pd_hi, lane);
-    flush_lens(ws, pd_s, pd_m, out_len, status, lane);
+    flush_lens(ws, pd_s, pd_m, out_len, status, lane, kGaps ? str_kind : nullptr);
   }
   TL(63);
 }
@@ -1566,7 +1617,8 @@ extern "C" int mhq_diag_timeline(unsigned long long *out, int n) {
 
 hipError_t launch_decode(const DevTables &t, const uint8_t *in, const uint64_t *in_off, uint64_t in_bias,
                          uint64_t n, uint8_t *out, const uint64_t *out_off, uint64_t out_bias,
-                         uint32_t *out_len, uint8_t *status, hipStream_t s, const uint64_t *in_end) {
+                         uint32_t *out_len, uint8_t *status, hipStream_t s, const uint32_t *in_end,
+                         const uint8_t *str_kind) {
   if (n == 0) return hipSuccess;
   // One workgroup per CU, each a contiguous range of whole wave tiles.  The
   // tile length (<= kTile) is chosen so that every wave gets the same number
@@ -1580,11 +1632,11 @@ hipError_t launch_decode(const DevTables &t, const uint8_t *in, const uint64_t *
   const uint64_t per_block = (((n + cus - 1) / cus + tl - 1) / tl) * tl;
   const unsigned grid = (unsigned)((n + per_block - 1) / per_block);
   if (in_end)
-    decode_kernel<true><<<dim3(grid), dim3(kT), 0, s>>>(in, in_off, in_end, in_bias, n, out, out_off, out_bias,
+    decode_kernel<true><<<dim3(grid), dim3(kT), 0, s>>>(in, in_off, in_end, str_kind, in_bias, n, out, out_off, out_bias,
                                                         out_len, status, t.lut1, t.lut2, t.len, per_block,
                                                         (uint32_t)tl);
   else
-    decode_kernel<false><<<dim3(grid), dim3(kT), 0, s>>>(in, in_off, nullptr, in_bias, n, out, out_off, out_bias,
+    decode_kernel<false><<<dim3(grid), dim3(kT), 0, s>>>(in, in_off, nullptr, nullptr, in_bias, n, out, out_off, out_bias,
                                                          out_len, status, t.lut1, t.lut2, t.len, per_block,
                                                          (uint32_t)tl);
   return hipGetLastError();

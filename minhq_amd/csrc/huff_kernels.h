@@ -35,13 +35,16 @@ hipError_t launch_offsets_sums(const uint32_t *enc_len, uint64_t n, uint64_t *bl
 hipError_t launch_encode(const DevTables &t, const uint8_t *in, const uint64_t *in_off,
                          uint64_t in_bias, uint64_t n, uint8_t *out, const uint64_t *out_off,
                          uint64_t out_bias, hipStream_t s);
-// in_end (optional): literal i is in[in_off[i] - in_bias .. in_end[i] - in_bias),
-// in_end[i] <= in_off[i + 1] when the literals are in order (any order decodes;
-// in-order tiles are the fast ones), in_off[n] >= every in_end.
+// in_end (optional): literal i is in[in_off[i] - in_bias .. e_i - in_bias), e_i
+// the first position at or after in_off[i] whose low 32 bits are in_end[i]
+// (literals under 4 GiB); e_i <= in_off[i + 1] when the literals are in order
+// (any order decodes; in-order tiles are the fast ones), in_off[n] >= every
+// e_i.  str_kind (with in_end: read_strings' framed strings, kind & 3 == 1
+// for Huffman): out_len / status get ReadString's outcome (str_outcome).
 hipError_t launch_decode(const DevTables &t, const uint8_t *in, const uint64_t *in_off,
                          uint64_t in_bias, uint64_t n, uint8_t *out, const uint64_t *out_off,
                          uint64_t out_bias, uint32_t *out_len, uint8_t *status, hipStream_t s,
-                         const uint64_t *in_end = nullptr);
+                         const uint32_t *in_end = nullptr, const uint8_t *str_kind = nullptr);
 // out_off[i] = base + sum_{j<i} enc_len[j]; cap_off[i] = base + sum_{j<i} floor(8*enc_len[j]/5)
 // (either output may be null).  Scratch: offsets_scratch_bytes(n) bytes, or
 // null for a hipMallocAsync on `s`.
@@ -60,6 +63,14 @@ hipError_t launch_offsets_pair(const uint32_t *a, const uint32_t *b, uint64_t n,
 hipError_t launch_offsets_pair_sums(const uint32_t *a, const uint32_t *b, uint64_t n, uint64_t *block_sums,
                                     uint64_t lim_a, uint64_t lim_b, uint64_t *oa, uint64_t *ob, hipStream_t s,
                                     const uint64_t *gate = nullptr, uint64_t gen = 0);
+// read_strings' fallback layout: out_off[i] = min(sum_{j<i} cap_j, lim), cap_j
+// the output capacity of framed string j recomputed from its parse (kind & 3:
+// 1 Huffman floor(8*take/5) with take the low word of hend - start, 0 raw
+// next - start, 2 none), over the per-kLenSumBlock sums its parse wrote; only
+// when *gate == gen.
+hipError_t launch_read_caps_sums(const uint64_t *start, const uint32_t *hend, const uint64_t *next,
+                                 const uint8_t *kind, uint64_t n, uint64_t *block_sums, uint64_t lim,
+                                 uint64_t *out_off, hipStream_t s, const uint64_t *gate, uint64_t gen);
 // cap_off[i] = base + sum_{j<i} floor(8*(in_off[j+1]-in_off[j])/5): decode capacities
 // for a batch whose encoded offsets are known.
 // Batch ReadString / WriteStringRaw (str_frame.hip); see include/mhq_huff.h.

@@ -117,6 +117,30 @@ struct PairVal {  // two independent u32 lengths -> two offset arrays (b null: o
   }
 };
 
+struct ReadCapVal {  // read_strings' framed strings -> output capacities (launch_read_caps_sums)
+  const uint64_t *start, *next;
+  const uint32_t *hend;
+  const uint8_t *kind;
+  uint64_t n;
+  __device__ inline void load(uint64_t i0, uint64_t *x, uint64_t *y) const {
+#pragma unroll
+    for (int k = 0; k < kItems; k++) {
+      const uint64_t i = i0 + k;
+      uint64_t c = 0;
+      if (i < n) {
+        const uint32_t kd = kind[i] & 3u;
+        const uint64_t st = start[i];
+        if (kd == 1u)
+          c = (uint64_t)(uint32_t)((uint64_t)(uint32_t)(hend[i] - (uint32_t)st) * 8u / 5u);
+        else if (kd == 0u)
+          c = (uint64_t)(uint32_t)(next[i] - st);
+      }
+      x[k] = c;
+      y[k] = 0;
+    }
+  }
+};
+
 __device__ inline uint64_t wave_sum(uint64_t x) {
 #pragma unroll
   for (int d = 1; d < kWave; d <<= 1) x += __shfl_xor(x, d);
@@ -230,7 +254,11 @@ __global__ __launch_bounds__(kScanBlock) void scan_apply_kernel(F f, uint64_t n,
   f.load(i0, a, b);
   const uint64_t first = (uint64_t)blockIdx.x * g;  // this chunk's first pair
   uint64_t pa = 0, pb = 0;
-  if (!sup) {
+#ifndef MHQ_X_SCAN  // timing experiments only (wrong output): 1 no prefix of the sums before the chunk, 2 no stores
+#define MHQ_X_SCAN 0
+#endif
+  if (MHQ_X_SCAN & 1) {
+  } else if (!sup) {
     // direct form (few sums, see direct_sums): the raw pairs before this
     // chunk's first, added up here; no second pass
     // (kDirectU loads per thread in flight at once: the pairs are L2 reads,
@@ -287,7 +315,9 @@ __global__ __launch_bounds__(kScanBlock) void scan_apply_kernel(F f, uint64_t n,
   }
   typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
   const uint64_t c0 = (uint64_t)blockIdx.x * kChunk;
-  if (c0 + kChunk <= n + 1) {
+  if (MHQ_X_SCAN & 2) {
+    if (xa[0] == 0x123456789ull) oa[0] = xb[kItems - 1];  // (keeps the values live)
+  } else if (c0 + kChunk <= n + 1) {
     // a whole chunk: through LDS, so each wave-wide 16-B store covers 1 KiB
     // of consecutive offsets (stores straight from the owning threads touch
     // 64 lines each)
@@ -407,6 +437,21 @@ hipError_t launch_offsets_pair_sums(const uint32_t *a, const uint32_t *b, uint64
   scan_apply_kernel<PairVal><<<dim3((unsigned)nb), dim3(kScanBlock), 0, s>>>(
       PairVal{a, b, n}, n, block_sums, direct ? nullptr : sup, (uint32_t)(kChunk / kLenSumBlock), 0, oa, ob, lim_a,
       lim_b, gate, gen);
+  return hipGetLastError();
+}
+
+hipError_t launch_read_caps_sums(const uint64_t *start, const uint32_t *hend, const uint64_t *next,
+                                 const uint8_t *kind, uint64_t n, uint64_t *block_sums, uint64_t lim,
+                                 uint64_t *out_off, hipStream_t s, const uint64_t *gate, uint64_t gen) {
+  const uint64_t nb = (n + 1 + kChunk - 1) / kChunk;
+  const uint64_t ns = (n + kLenSumBlock - 1) / kLenSumBlock;
+  const uint64_t nsup = sup_count(ns);
+  uint64_t *sup = block_sums + 2 * (ns + 1);
+  const bool direct = direct_sums(nb, ns);
+  if (!direct) scan_sums_kernel<<<dim3((unsigned)nsup), dim3(kScanBlock), 0, s>>>(block_sums, ns, sup);
+  scan_apply_kernel<ReadCapVal><<<dim3((unsigned)nb), dim3(kScanBlock), 0, s>>>(
+      ReadCapVal{start, next, hend, kind, n}, n, block_sums, direct ? nullptr : sup, (uint32_t)(kChunk / kLenSumBlock),
+      0, out_off, nullptr, lim, lim, gate, gen);
   return hipGetLastError();
 }
 

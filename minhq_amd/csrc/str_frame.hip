@@ -26,10 +26,17 @@ inline unsigned blocks(uint64_t n) { return (unsigned)((n + kT - 1) / kT); }
 // Per-string parse state between the read kernels.
 struct ReadScratch {
   uint64_t *start;  // payload start (byte index into blk); start[n] = blk_len (the decode's in_off)
-  uint64_t *hend;   // Huffman payload end: start + take for a Huffman string, start otherwise (in_end)
-  uint32_t *cap;    // output capacity: floor(8*take/5) (Huffman) or take (raw)
+  uint32_t *hend;   // low word of the Huffman payload end: start + take for a Huffman string, start
+                    // otherwise (the decode's in_end)
   uint8_t *kind;    // 0 raw, 1 Huffman, 2 header error (hc/io.go:74-81 return ("", nil)); | kDeclared
 };
+// A string's output capacity, recomputed from its parse where it is needed
+// (the fallback layout, a cut region): floor(8*take/5) (Huffman), take (raw).
+__device__ __forceinline__ uint64_t read_cap(uint8_t kind, uint64_t start, uint32_t hend, uint64_t next) {
+  const uint32_t k = kind & 3u;
+  if (k == 1u) return (uint32_t)((uint64_t)(uint32_t)(hend - (uint32_t)start) * 8u / 5u);
+  return k == 0u ? (uint32_t)(next - start) : 0u;
+}
 constexpr uint8_t kDeclared = 4;  // the declared length is not 0
 
 // Reader.ReadBit + Reader.ReadInt(prefix) at byte pos, bit 7-prefix being the
@@ -57,7 +64,7 @@ __global__ __launch_bounds__(kT) void read_parse_kernel(const uint8_t *__restric
                                                         ReadScratch sc, uint64_t *__restrict__ next,
                                                         uint64_t *__restrict__ block_sums,
                                                         uint64_t *__restrict__ out_off, uint64_t *order_bad,
-                                                        uint64_t gen) {
+                                                        uint64_t *finish_needed, uint64_t gen) {
   static_assert(kT == kLenSumBlock, "block sums per kLenSumBlock strings: one per k");
   // Every load of the thread's strings is issued before the first one is
   // used (the per-string chain pos -> header octet is two dependent loads).
@@ -76,7 +83,7 @@ __global__ __launch_bounds__(kT) void read_parse_kernel(const uint8_t *__restric
 #pragma unroll
   for (int k = 0; k < kParsePer; k++) b0[k] = p0[k] < lim[k] ? blk[p0[k]] : 0u;
   uint32_t caps[kParsePer];
-  bool bad = false;
+  bool bad = false, raw = false;
 #pragma unroll
   for (int k = 0; k < kParsePer; k++) {
     const uint64_t i = i0 + (uint64_t)k * kT;
@@ -117,11 +124,11 @@ __global__ __launch_bounds__(kT) void read_parse_kernel(const uint8_t *__restric
     // placed at min(pos, blk_len) -- every start stays inside [0, blk_len]
     start = start < blk_len ? start : blk_len;
     sc.start[i] = start;
-    sc.hend[i] = kind == 1 ? start + take : start;
+    sc.hend[i] = (uint32_t)(kind == 1 ? start + take : start);
     if (i == n - 1) sc.start[n] = blk_len;
     sc.kind[i] = kind | (kind != 2 && v != 0 ? kDeclared : 0);
     caps[k] = kind == 1 ? (uint32_t)(take * 8 / 5) : (uint32_t)take;
-    sc.cap[i] = caps[k];
+    raw |= kind == 0;
     next[i] = kind == 2 ? p0[k] : start + take;
     // the region at the scaled payload start; in block order the next one
     // starts at or after scaled(start + take) (its payload starts after its
@@ -131,6 +138,7 @@ __global__ __launch_bounds__(kT) void read_parse_kernel(const uint8_t *__restric
     bad |= start + take > min(pn[k], blk_len);
   }
   if (bad) *order_bad = gen;  // (rare: every writer stores the same value)
+  if (raw) *finish_needed = gen;  // raw payloads to copy: the finish pass runs
   // (sum of cap, sum of cap) per kLenSumBlock strings: group k of this block
   __shared__ uint64_t part[kParsePer][kT / 64];
   const uint32_t lane = threadIdx.x % 64, wave = threadIdx.x / 64;
@@ -196,19 +204,23 @@ __device__ __forceinline__ void copy_bytes(uint8_t *__restrict__ dst, const uint
 
 // Raw payloads into the output (after the decode), then the per-string
 // outcome of hc/io.go:92-96.  The decode has written out_len / status for
-// every string (0 / OK for the raw and unreadable ones, which it sees as
-// empty literals), so only the strings whose outcome differs are written:
-// INVALID (length 0), EOF, raw payloads and cut regions.  Regions are cut
-// short only at the output's end (the scan clamps the offsets to out_cap), so
-// with out_off[n] < out_cap no region is and the capacity test reads nothing.
+// every string, with the Huffman strings' outcome applied (INVALID length 0,
+// EOF: str_outcome), 0 / OK for the raw and unreadable ones (empty literals
+// to it), so only raw payloads, raw EOFs and cut regions are left.  Regions
+// are cut short only at the output's end (the scan clamps the offsets to
+// out_cap), so with out_off[n] < out_cap no region is and the capacity test
+// reads nothing; with no raw string either (the parse stores `gen` to
+// *finish_needed otherwise) the pass ends at once.
 __global__ __launch_bounds__(kT) void read_finish_kernel(const uint8_t *__restrict__ blk, ReadScratch sc, uint64_t n,
                                                          const uint64_t *__restrict__ out_off,
                                                          const uint64_t *__restrict__ next,
                                                          uint8_t *__restrict__ out, uint32_t *__restrict__ out_len,
-                                                         uint8_t *__restrict__ status, uint64_t out_cap) {
+                                                         uint8_t *__restrict__ status, uint64_t out_cap,
+                                                         const uint64_t *finish_needed, uint64_t gen) {
+  const bool clamped = out_off[n] >= out_cap;  // (uniform)
+  if (!clamped && __builtin_nontemporal_load(finish_needed) != gen) return;
   // kParsePer strings per thread as in read_parse_kernel, all loads first
   const uint64_t i0 = (uint64_t)blockIdx.x * (kT * kParsePer) + threadIdx.x;
-  const bool clamped = out_off[n] >= out_cap;  // (uniform)
   uint8_t kd[kParsePer], ds[kParsePer];
   uint64_t o0[kParsePer], o1[kParsePer];
   uint32_t cap[kParsePer], dl[kParsePer];
@@ -224,7 +236,7 @@ __global__ __launch_bounds__(kT) void read_finish_kernel(const uint8_t *__restri
     if (clamped) {
       o0[k] = out_off[j];
       o1[k] = out_off[j + 1];
-      cap[k] = sc.cap[j];
+      cap[k] = (uint32_t)read_cap(kd[k], sc.start[j], sc.hend[j], next[j]);
     }
   }
 #pragma unroll
@@ -522,7 +534,7 @@ namespace {
 
 // read_strings' scratch, 16-B aligned pieces of one allocation.
 struct ReadLayout {
-  size_t start, hend, cap, kind, order_bad, sums, total;
+  size_t start, hend, kind, flags, sums, total;
   ReadLayout(uint64_t n, uint64_t blk_len) {
     size_t o = 0;
     auto take_ = [&](size_t bytes) {
@@ -531,10 +543,9 @@ struct ReadLayout {
       return at;
     };
     start = take_(8 * (n + 1));
-    hend = take_(8 * n);
-    cap = take_(4 * n);
+    hend = take_(4 * n);
     kind = take_(n);
-    order_bad = take_(8);
+    flags = take_(16);  // order_bad, finish_needed
     sums = take_(offsets_sums_scratch_bytes(n));
     total = o;
   }
@@ -563,26 +574,27 @@ hipError_t launch_read_strings(const DevTables &t, const uint8_t *blk, uint64_t 
   uint8_t *base = (uint8_t *)scratch;
   hipError_t e = hipSuccess;
   if (!base && (e = hipMallocAsync((void **)&base, L.total, s)) != hipSuccess) return e;
-  ReadScratch sc{(uint64_t *)(base + L.start), (uint64_t *)(base + L.hend), (uint32_t *)(base + L.cap),
-                 base + L.kind};
+  ReadScratch sc{(uint64_t *)(base + L.start), (uint32_t *)(base + L.hend), base + L.kind};
+  uint64_t *order_bad = (uint64_t *)(base + L.flags), *finish_needed = order_bad + 1;
+  // (one generation number per call: the flags are set by storing it, never
+  // cleared, so a stale scratch cannot gate this call's passes)
+  static std::atomic<uint64_t> g_gen{0};
+  const uint64_t gen = 0x6d68712000000000ull + g_gen.fetch_add(1, std::memory_order_relaxed) + 1;
 #define TRY(x)                   \
   do {                           \
     e = (x);                     \
     if (e != hipSuccess) goto done; \
   } while (0)
-  {
-    static std::atomic<uint64_t> g_gen{0};
-    const uint64_t gen = 0x6d68712000000000ull + g_gen.fetch_add(1, std::memory_order_relaxed) + 1;
-    uint64_t *order_bad = (uint64_t *)(base + L.order_bad);
-    read_parse_kernel<<<(unsigned)((n + kT * kParsePer - 1) / (kT * kParsePer)), kT, 0, s>>>(
-        blk, blk_len, pos, limit, prefix, n, sc, next, (uint64_t *)(base + L.sums), out_off, order_bad, gen);
-    TRY(hipGetLastError());
-    // strings out of block order: capacities back to back instead
-    TRY(launch_offsets_pair_sums(sc.cap, nullptr, n, (uint64_t *)(base + L.sums), out_cap, out_cap, out_off,
-                                 nullptr, s, order_bad, gen));
-  }
-  TRY(launch_decode(t, blk, sc.start, 0, n, out, out_off, 0, out_len, status, s, sc.hend));
-  read_finish_kernel<<<(unsigned)((n + kT * kParsePer - 1) / (kT * kParsePer)), kT, 0, s>>>(blk, sc, n, out_off, next, out, out_len, status, out_cap);
+  read_parse_kernel<<<(unsigned)((n + kT * kParsePer - 1) / (kT * kParsePer)), kT, 0, s>>>(
+      blk, blk_len, pos, limit, prefix, n, sc, next, (uint64_t *)(base + L.sums), out_off, order_bad, finish_needed,
+      gen);
+  TRY(hipGetLastError());
+  // strings out of block order: capacities back to back instead
+  TRY(launch_read_caps_sums(sc.start, sc.hend, next, sc.kind, n, (uint64_t *)(base + L.sums), out_cap, out_off, s,
+                            order_bad, gen));
+  TRY(launch_decode(t, blk, sc.start, 0, n, out, out_off, 0, out_len, status, s, sc.hend, sc.kind));
+  read_finish_kernel<<<(unsigned)((n + kT * kParsePer - 1) / (kT * kParsePer)), kT, 0, s>>>(
+      blk, sc, n, out_off, next, out, out_len, status, out_cap, finish_needed, gen);
   TRY(hipGetLastError());
 done:
   if (!scratch) {

@@ -429,3 +429,85 @@ def test_encode_empty_region_skips_literal(codec, oracle_mod):
     ref = b"".join(oracle_mod.encode(x) for x, k in zip(lits, keep) if k)
     assert got[: int(oo[-1])].tobytes() == ref
     assert (got[int(oo[-1]):] == 0xAB).all()
+
+
+class _Pinned:
+    """Allocator of pinned (page-locked) host buffers for the host entry
+    points: with every buffer pinned the kernels read and write them in place
+    over PCIe (mhq_api.cpp run_zero_copy) instead of staging copies.
+    `at_end`: each buffer ends exactly at the end of its pinned block, so an
+    input has no slack past it and the call takes the staged path."""
+
+    def __init__(self, at_end=False):
+        self.at_end, self.keep = at_end, []
+
+    def block(self, nbytes):
+        import torch
+
+        size = 1 << max(12, (max(nbytes, 1) - 1).bit_length())  # torch's pinned blocks are powers of two
+        t = torch.empty(size, dtype=torch.uint8).pin_memory()
+        self.keep.append(t)
+        a = t.numpy()
+        return a[size - nbytes:] if self.at_end else a[:nbytes]
+
+    def __call__(self, nbytes):
+        return self.block(nbytes)
+
+    def copy(self, arr):
+        arr = np.ascontiguousarray(arr)
+        b = self.block(arr.nbytes).view(arr.dtype)
+        b[:] = arr
+        return b
+
+
+@pytest.mark.parametrize("at_end", [False, True])
+@pytest.mark.parametrize("dist", ["hdr", "adv", "zipf"])
+def test_pinned_host_buffers_vs_oracle(codec, oracle_mod, dist, at_end):
+    """Host entry points on pinned buffers (in place over PCIe; staged when
+    the inputs end at their block's end) vs the oracle, bit-exact: encode_len,
+    encode, decode, including bytes past each out_len left untouched."""
+    from minhq_amd import hc, workloads
+
+    if dist == "zipf":
+        b = workloads.make_batch(30000, "zipf", "hdr", workloads.SEED_ZIPF)
+    else:
+        lo, hi = (128, 128) if dist == "adv" else (0, 64)
+        b = workloads.make_batch(20000, "fixed" if dist == "adv" else "uniform", dist, lo=lo, hi=hi)
+    P = _Pinned(at_end)
+    data, off = P.copy(b.data), P.copy(b.off)
+    enc_len_ref, enc_ref, eoff = _oracle_encode_batch(oracle_mod, b.data, b.off)
+    assert np.array_equal(codec.encode_len(data, off, alloc=P), enc_len_ref)
+    enc, eoff_gpu = codec.encode(data, off, alloc=P)
+    assert np.array_equal(eoff_gpu, eoff)
+    assert enc.tobytes() == enc_ref.tobytes()
+    cap = hc.capacity_offsets(eoff)
+    out_ref, len_ref, st_ref = oracle_mod.decode_batch(enc_ref, eoff, cap, nthreads=8)
+    out, _, out_len, status = codec.decode(P.copy(enc_ref), P.copy(eoff), P.copy(cap), alloc=P)
+    assert np.array_equal(out_len, len_ref)
+    assert np.array_equal(status, st_ref)
+    starts = cap[:-1].astype(np.int64)
+    lens = len_ref.astype(np.int64)
+    idx = np.repeat(starts, lens) + (np.arange(lens.sum()) - np.repeat(np.cumsum(lens) - lens, lens))
+    assert np.array_equal(out[idx], b.data)
+
+
+def test_pinned_host_garbage_and_bias(codec, oracle_mod):
+    """In-place decode of arbitrary bytes (INVALID, truncation) with offsets
+    that do not start at 0, against the oracle."""
+    from minhq_amd import hc
+
+    rng = np.random.default_rng(11)
+    lens = rng.integers(0, 90, 5000)
+    off = np.zeros(len(lens) + 1, dtype=np.uint64)
+    off[1:] = np.cumsum(lens)
+    enc = rng.integers(0, 256, int(off[-1]), dtype=np.uint8)
+    cap = hc.capacity_offsets(off)
+    out_ref, len_ref, st_ref = oracle_mod.decode_batch(enc, off, cap, nthreads=8)
+    P = _Pinned()
+    bias, cbias = np.uint64(4093), np.uint64(37)
+    out, _, out_len, status = codec.decode(P.copy(enc), P.copy(off + bias), P.copy(cap + cbias), alloc=P)
+    assert np.array_equal(out_len, len_ref)
+    assert np.array_equal(status, st_ref)
+    for i in range(0, len(lens), 7):
+        a = int(cap[i])
+        assert out[a: a + int(out_len[i])].tobytes() == out_ref[a: a + int(len_ref[i])].tobytes()
