@@ -64,8 +64,18 @@ const char *mhq_strerror(int rc);
 int mhq_code_table(uint8_t *len, uint32_t *code);
 
 /* ---------------- host-memory batches (PCIe-inclusive path) ---------------
- * The batch is sharded over the context's devices by encoded bytes; each shard
- * is copied in, processed and copied back.  Synchronous. */
+ * The batch is sharded over the context's devices by encoded bytes.  When
+ * every buffer of a call is pinned, device-mapped host memory (mhq_host_alloc,
+ * hipHostMalloc, torch pin_memory) the kernels read and write it in place
+ * over PCIe, one launch per shard; otherwise (pageable memory) each shard is
+ * copied in, processed and copied back in pipelined chunks.  Synchronous. */
+
+/* Pinned, device-mapped host memory for the host-memory calls: buffers from
+ * here take the in-place route (no Go/C heap buffer can).  NULL when the
+ * allocation fails or no device is visible.  A replacement for the C.malloc
+ * of the cgo shim; free with mhq_host_free. */
+void *mhq_host_alloc(size_t bytes);
+void mhq_host_free(void *p);
 
 /* enc_len[i] = encoded bytes of literal i = ceil(sum of code lengths / 8).
  * Replaces the sizing done by bytes.Buffer in hc/io.go:157-171; drives the

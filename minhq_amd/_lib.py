@@ -46,6 +46,8 @@ SIGNATURES = {
     "mhq_device_count": (C.c_int, [vp]),
     "mhq_strerror": (C.c_char_p, [C.c_int]),
     "mhq_code_table": (C.c_int, [u8p, u32p]),
+    "mhq_host_alloc": (vp, [C.c_size_t]),
+    "mhq_host_free": (None, [vp]),
     "mhq_huff_encode_len": (C.c_int, [vp, u8p, u64p, C.c_uint64, u32p]),
     "mhq_huff_encode": (C.c_int, [vp, u8p, u64p, C.c_uint64, u8p, u64p]),
     "mhq_huff_decode": (C.c_int, [vp, u8p, u64p, C.c_uint64, u8p, u64p, u32p, u8p]),

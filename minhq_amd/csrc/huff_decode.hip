@@ -464,6 +464,60 @@ struct WinBuf {
     return (x << (pa & 31u)) | ((uint64_t)(uint32_t)(0xffffffffull >> c) << 32);
   }
 };
+// MHQ_DEC_WIN 3: the window as its top 32 bits only, one v_alignbit of the
+// two staged words (no 64-bit shift, no word swap).  The state is the bit
+// address minus one, so the words are those holding bits p-1 and p+31 and the
+// shift ~pm & 31 is 31 - ((p-1) & 31): 0 when p is word-aligned (the second
+// word whole), the first word's low bits otherwise.  Both probes and the stop
+// test read these 32 bits (a first code takes at most 12, the second probe
+// 12 more; a long code at most 30).
+struct WinBuf3 {
+  uint32_t pm;   // LDS bit address of the next bit, minus 1
+  int32_t left;  // endbit - p
+  uint32_t msk;  // ones from bit `left` on (MSB first): set with left, off the next step's read
+  __device__ __forceinline__ void set_mask() { msk = (uint32_t)(0xffffffffull >> (uint32_t)min(max(left, 0), 32)); }
+  __device__ __forceinline__ void init(const uint32_t *words, uint32_t p0, uint32_t endbit) {
+    pm = 8u * (uint32_t)(uintptr_t)words + p0 - 1u;
+    left = (int32_t)(endbit - p0);
+    set_mask();
+  }
+  __device__ __forceinline__ uint32_t top() const {
+    typedef __attribute__((address_space(3))) const uint32_t lds_u32;
+    lds_u32 *w = (lds_u32 *)(uintptr_t)((pm >> 3) & ~3u);
+    return __builtin_amdgcn_alignbit(w[0], w[1], ~pm) | msk;
+  }
+};
+
+template <bool kLong = true>
+__device__ __forceinline__ bool win_step32(const Smem &sm, WinBuf3 &in, OutAccL &out, PendL &pend, bool &stop) {
+  const uint32_t S = in.top();
+  stop = S >= 0xfffffffcu;
+  uint32_t e = sm.lut1[S >> (32 - kLut1Bits)];
+  atomicOr(pend.p, pend.v);
+  bool lng = false;
+  if (kLong && ((e == 0u) & !stop)) {  // a code of 13..29 bits (one branch: no short circuit)
+    uint32_t sym = 0;
+    const uint32_t L = long_code(sm.lut2, S, sym);
+    e = L | (8u << 8) | (sym << 16);
+    lng = true;
+  }
+  out.put(e >> 16, (e >> 8) & 0xffu);
+  uint32_t e2 = sm.lut1[(S << (e & 31u)) >> (32 - kLut1Bits)];
+  e2 = lng ? 0u : e2;
+  out.put(e2 >> 16, (e2 >> 8) & 0xffu);
+  const uint32_t n = (e & 0xffu) + (e2 & 0xffu);
+  in.pm += n;
+  in.left -= (int32_t)n;
+  in.set_mask();
+  pend.p = out.op;
+  pend.v = (uint32_t)out.acc;
+  const uint32_t t = out.ab & 32u;
+  out.acc >>= t;
+  out.op += t >> 5;
+  out.ab &= 31u;
+  return stop || in.left < 0;
+}
+
 template <bool kLong = true, class WB>
 __device__ __forceinline__ bool win_step(const Smem &sm, const uint32_t *words, WB &in, OutAccL &out,
                                          PendL &pend, bool &stop) {
@@ -908,7 +962,13 @@ __device__ __forceinline__ void decode_piece(const Smem &sm, WaveSmem &ws, uint3
   }
 #elif MHQ_DEC_WIN
   {
+#if MHQ_DEC_WIN == 3
+    WinBuf3 in;
+#define MHQ_WSTEP(K) win_step32<K>(sm, in, out, pend, stop)
+#else
     WinBuf in;
+#define MHQ_WSTEP(K) win_step<K>(sm, ws.in_w, in, out, pend, stop)
+#endif
     in.init(ws.in_w, roomA ? A.p : B.p, roomA ? A.endbit : B.endbit);
     OutAccL out;
     out.init(ws.out_w, roomA ? A.optr : B.optr);
@@ -918,8 +978,8 @@ __device__ __forceinline__ void decode_piece(const Smem &sm, WaveSmem &ws, uint3
     while (active) {
       bool stop;
 #pragma unroll
-      for (int k = 1; k < MHQ_DEC_STEPS; k++) win_step<MHQ_DEC_LONG1 != 0>(sm, ws.in_w, in, out, pend, stop);
-      if (win_step(sm, ws.in_w, in, out, pend, stop)) {
+      for (int k = 1; k < MHQ_DEC_STEPS; k++) MHQ_WSTEP(MHQ_DEC_LONG1 != 0);
+      if (MHQ_WSTEP(true)) {
         const uint32_t r = in.left < 0 ? kRedo : (out.optr(ws.out_w) - ost) | ((uint32_t)(in.left > kEosOnes) << 31);
         rA = onB ? rA : r;
         rB = onB ? r : rB;
@@ -931,6 +991,7 @@ __device__ __forceinline__ void decode_piece(const Smem &sm, WaveSmem &ws, uint3
       }
     }
     atomicOr(pend.p, pend.v);
+#undef MHQ_WSTEP
   }
 #else
   {

@@ -559,6 +559,21 @@ const char *mhq_strerror(int rc) {
   }
 }
 
+void *mhq_host_alloc(size_t bytes) {
+  // kZcSlack more than asked: an input that ends where the caller's buffer
+  // ends still has the slack the in-place route wants after it
+  void *p = nullptr;
+  if (hipHostMalloc(&p, bytes + kZcSlack, hipHostMallocDefault) != hipSuccess) {
+    (void)hipGetLastError();
+    return nullptr;
+  }
+  return p;
+}
+
+void mhq_host_free(void *p) {
+  if (p) (void)hipHostFree(p);
+}
+
 int mhq_code_table(uint8_t *len, uint32_t *code) {
   const mhq::Tables *t = tables();
   if (!t || !len || !code) return MHQ_EINVAL;

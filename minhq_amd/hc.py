@@ -78,6 +78,39 @@ def _p(a: np.ndarray, t):
     return a.ctypes.data_as(C.POINTER(t))
 
 
+def pinned_empty(nbytes: int) -> np.ndarray:
+    """A uint8 array in pinned, device-mapped host memory (mhq_host_alloc):
+    host-memory calls whose buffers are all such arrays run in place (the
+    kernels read and write them over PCIe).  Freed with the
+    array."""
+    import weakref
+
+    L = _lib.load()
+    n = max(int(nbytes), 1)
+    p = L.mhq_host_alloc(n)
+    if not p:
+        raise MemoryError(f"mhq_host_alloc({n}) failed")
+    buf = (C.c_uint8 * n).from_address(p)
+    weakref.finalize(buf, L.mhq_host_free, p)
+    return np.frombuffer(buf, dtype=np.uint8)[: int(nbytes)]
+
+
+def pinned_copy(a: np.ndarray) -> np.ndarray:
+    """`a` copied into pinned_empty memory (same dtype and shape)."""
+    a = np.ascontiguousarray(a)
+    out = pinned_empty(a.nbytes).view(a.dtype).reshape(a.shape)
+    out[...] = a
+    return out
+
+
+class PinnedAllocator:
+    """`alloc=` for the Codec's host-memory methods: every output in pinned
+    memory (pinned_empty), so with pinned inputs the call runs in place."""
+
+    def __call__(self, nbytes: int) -> np.ndarray:
+        return pinned_empty(nbytes)
+
+
 def _alloc(alloc, n: int, dtype) -> np.ndarray:
     if alloc is None:
         return np.zeros(n, dtype=dtype)

@@ -436,12 +436,18 @@ class _Pinned:
     points: with every buffer pinned the kernels read and write them in place
     over PCIe (mhq_api.cpp run_zero_copy) instead of staging copies.
     `at_end`: each buffer ends exactly at the end of its pinned block, so an
-    input has no slack past it and the call takes the staged path."""
+    input has no slack past it and the call takes the staged path.
+    `mhq`: the buffers come from the ABI's own mhq_host_alloc (hc.pinned_empty)
+    instead of torch."""
 
-    def __init__(self, at_end=False):
-        self.at_end, self.keep = at_end, []
+    def __init__(self, at_end=False, mhq=False):
+        self.at_end, self.mhq, self.keep = at_end, mhq, []
 
     def block(self, nbytes):
+        if self.mhq:
+            from minhq_amd import hc
+
+            return hc.pinned_empty(nbytes)
         import torch
 
         size = 1 << max(12, (max(nbytes, 1) - 1).bit_length())  # torch's pinned blocks are powers of two
@@ -460,9 +466,9 @@ class _Pinned:
         return b
 
 
-@pytest.mark.parametrize("at_end", [False, True])
+@pytest.mark.parametrize("source", ["torch", "torch_at_end", "mhq"])
 @pytest.mark.parametrize("dist", ["hdr", "adv", "zipf"])
-def test_pinned_host_buffers_vs_oracle(codec, oracle_mod, dist, at_end):
+def test_pinned_host_buffers_vs_oracle(codec, oracle_mod, dist, source):
     """Host entry points on pinned buffers (in place over PCIe; staged when
     the inputs end at their block's end) vs the oracle, bit-exact: encode_len,
     encode, decode, including bytes past each out_len left untouched."""
@@ -473,7 +479,7 @@ def test_pinned_host_buffers_vs_oracle(codec, oracle_mod, dist, at_end):
     else:
         lo, hi = (128, 128) if dist == "adv" else (0, 64)
         b = workloads.make_batch(20000, "fixed" if dist == "adv" else "uniform", dist, lo=lo, hi=hi)
-    P = _Pinned(at_end)
+    P = _Pinned(at_end=source == "torch_at_end", mhq=source == "mhq")
     data, off = P.copy(b.data), P.copy(b.off)
     enc_len_ref, enc_ref, eoff = _oracle_encode_batch(oracle_mod, b.data, b.off)
     assert np.array_equal(codec.encode_len(data, off, alloc=P), enc_len_ref)
