@@ -181,5 +181,58 @@ inline unsigned tile_grid(uint64_t ntiles, int waves, int per_cu) {
   return (unsigned)(want < cap ? want : cap);
 }
 
+
+// ---- read_strings' framed strings (str_frame.hip; finished in the decode) --
+// kind: 0 raw, 1 Huffman, 2 header error (hc/io.go:74-81 return ("", nil)),
+// | kDeclared when the declared length is not 0.
+constexpr uint8_t kDeclared = 4;
+// A string's output capacity, recomputed from its parse where it is needed
+// (the fallback layout, a cut region): floor(8*take/5) (Huffman), take (raw).
+__device__ __forceinline__ uint64_t read_cap(uint8_t kind, uint64_t start, uint32_t hend, uint64_t next) {
+  const uint32_t k = kind & 3u;
+  if (k == 1u) return (uint32_t)((uint64_t)(uint32_t)(hend - (uint32_t)start) * 8u / 5u);
+  return k == 0u ? (uint32_t)(next - start) : 0u;
+}
+
+// len bytes from src to dst, any alignments, by one thread: the 0-3 bytes up
+// to dst's first dword boundary and the 0-3 after its last whole dword go as
+// bytes (neighbouring bytes untouched), the middle as dword stores of source
+// dwords realigned with v_alignbyte.  Every load of a 64-byte block is issued
+// before its first store (no load-store round trip per word).  A source dword
+// read holds at least one byte of [src, src + len): inside any 4-B aligned
+// allocation.
+__device__ __forceinline__ void copy_bytes(uint8_t *__restrict__ dst, const uint8_t *__restrict__ src,
+                                           uint64_t len) {
+  const uint32_t h = (uint32_t)min((uint64_t)((0u - (uint32_t)(uintptr_t)dst) & 3u), len);
+  const uint64_t body = (len - h) & ~(uint64_t)3;
+  const uint32_t t = (uint32_t)(len - h) & 3u;
+  uint32_t hb[3], tb[3];
+#pragma unroll
+  for (uint32_t k = 0; k < 3; k++) {
+    hb[k] = k < h ? src[k] : 0u;
+    tb[k] = k < t ? src[h + body + k] : 0u;
+  }
+  const uint8_t *s1 = src + h;
+  uint32_t *d4 = (uint32_t *)(dst + h);
+  const uint32_t r = (uint32_t)(uintptr_t)s1 & 3u;
+  const uint32_t *w = (const uint32_t *)(s1 - r);
+  const uint64_t nw = body >> 2;
+  for (uint64_t q0 = 0; q0 < nw; q0 += 16) {
+    const uint32_t nq = (uint32_t)min(nw - q0, (uint64_t)16);
+    const uint32_t nload = nq + (r != 0u);
+    uint32_t x[17];
+#pragma unroll
+    for (uint32_t j = 0; j < 17; j++) x[j] = j < nload ? w[q0 + j] : 0u;
+#pragma unroll
+    for (uint32_t j = 0; j < 16; j++)
+      if (j < nq) d4[q0 + j] = __builtin_amdgcn_alignbyte(x[j + 1], x[j], r);
+  }
+#pragma unroll
+  for (uint32_t k = 0; k < 3; k++) {
+    if (k < h) dst[k] = (uint8_t)hb[k];
+    if (k < t) dst[h + body + k] = (uint8_t)tb[k];
+  }
+}
+
 }  // namespace dev
 }  // namespace mhq

@@ -438,8 +438,8 @@ __device__ __forceinline__ bool masked_step_lean(const Smem &sm, BitBufL &in, Ou
   return stop || in.left < 0;
 }
 
-#ifndef MHQ_DEC_WIN  // 1: the lean loop reads each step's 64-bit window afresh (no refill state)
-#define MHQ_DEC_WIN 1
+#ifndef MHQ_DEC_WIN  // 1: the lean loop reads each step's 64-bit window afresh (no refill state); 3: its top 32 bits by v_alignbit
+#define MHQ_DEC_WIN 3
 #endif
 // A literal's stream with no refill state: each step reads the two staged
 // words holding bit p (one ds_read2) and shifts them to a window of >= 33
@@ -794,7 +794,8 @@ __device__ __forceinline__ void put_chunk(WaveSmem &ws, uint32_t c, u32x4 v) {
 // (Raw and unreadable strings are empty literals here: 0 / OK, as the
 // reference returns for the unreadable ones; raw payloads are the finish
 // pass's.)
-constexpr uint32_t kStrEof = 2;  // MHQ_STR_EOF (include/mhq_huff.h)
+constexpr uint32_t kStrEof = 2;      // MHQ_STR_EOF (include/mhq_huff.h)
+constexpr uint32_t kStrNoSpace = 3;  // MHQ_STR_NOSPACE
 __device__ __forceinline__ void str_outcome(const uint8_t *__restrict__ str_kind, uint64_t i, uint32_t &len,
                                             uint32_t &st) {
   if (st != 0u)
@@ -1455,8 +1456,7 @@ __device__ void decode_tile_pieces(const Smem &sm, WaveSmem &ws, const uint8_t *
 // its len slot until the results overwrite it.
 template <bool kGaps>
 __global__ __launch_bounds__(kT) void decode_kernel(const uint8_t *__restrict__ in, const uint64_t *__restrict__ in_off,
-                                                    const uint32_t *__restrict__ in_end,
-                                                    const uint8_t *__restrict__ str_kind,
+                                                    const uint32_t *__restrict__ in_end, StrFinish str,
                                                     uint64_t in_bias, uint64_t n, uint8_t *__restrict__ out,
                                                     const uint64_t *__restrict__ out_off, uint64_t out_bias,
                                                     uint32_t *__restrict__ out_len, uint8_t *__restrict__ status,
@@ -1486,6 +1486,9 @@ __global__ __launch_bounds__(kT) void decode_kernel(const uint8_t *__restrict__ 
   // (Every wave loads them, as scalar loads, and waits for them only where
   // they are used: a load under `tid == 0` waited at once.)
   const uint64_t bnd[4] = {in_off[n], in_off[0], out_off[n], out_off[0]};
+  // read_strings: whether this workgroup finishes its range at the end (its
+  // gate word loaded now, used there)
+  const uint64_t fin_gate = kGaps && str.finish_needed ? __builtin_nontemporal_load(str.finish_needed) : 0;
 #if MHQ_DEC_SOPEN
   // The first tile's input range comes from two scalar loads (the tile's first
   // and one-past-last literal), so its input loads are issued without waiting
@@ -1527,8 +1530,15 @@ __global__ __launch_bounds__(kT) void decode_kernel(const uint8_t *__restrict__ 
   if (tid == 0) {
     const uint64_t nin = bnd[0] - bnd[1], nout = bnd[2] - bnd[3];
     const uint64_t ain = (nin + n - 1) / n, aout = (nout + n - 1) / n;
-    const uint64_t fit_in = (uint64_t)(kWIn - 16) * 4u / (5u * ain + 8u);
-    const uint64_t fit_out = (uint64_t)(kWOut - 16) * 4u / (5u * aout + 8u);
+    // kGaps (read_strings): a 20 % margin, not 25: its means include the
+    // frame headers and the scaled regions' slack (config 2: 27.5 and 44 B
+    // against 26.5 and 42.4), and a tile length cut below tl0 gives some
+    // waves a fourth tile (decode 41.9 against 35.3 us); tile sums of 114
+    // literals spread by ~4 %, so 20 % is still five deviations
+    const uint64_t fit_in = kGaps ? (uint64_t)(kWIn - 16) * 5u / (6u * ain + 10u)
+                                  : (uint64_t)(kWIn - 16) * 4u / (5u * ain + 8u);
+    const uint64_t fit_out = kGaps ? (uint64_t)(kWOut - 16) * 5u / (6u * aout + 10u)
+                                   : (uint64_t)(kWOut - 16) * 4u / (5u * aout + 8u);
     const uint64_t fit = min(fit_in, fit_out);
     sm.tl = fit >= (uint64_t)kWave && fit < (uint64_t)tl0 ? (uint32_t)fit : tl0;
   }
@@ -1608,7 +1618,7 @@ __global__ __launch_bounds__(kT) void decode_kernel(const uint8_t *__restrict__ 
       wave_sync();
       store_out(pd_o, (const uint8_t *)ws.out_w, pd_lo, pd_hi, lane);
 #endif
-      flush_lens(ws, pd_s, pd_m, out_len, status, lane, kGaps ? str_kind : nullptr);
+      flush_lens(ws, pd_s, pd_m, out_len, status, lane, kGaps ? str.kind : nullptr);
     }
     pd_o = nullptr;
     wave_sync();
@@ -1643,7 +1653,7 @@ __global__ __launch_bounds__(kT) void decode_kernel(const uint8_t *__restrict__ 
         decode_tile_pieces(sm, ws, in, in_off, in_bias, out, out_off, out_bias, out_len, status, s, cnt, lane);
       else
         decode_tile_long<kGaps>(sm, ws, in, in_off, in_end, in_bias, out, out_off, out_bias, out_len, status, s,
-                                cnt, lane, kGaps ? str_kind : nullptr);
+                                cnt, lane, kGaps ? str.kind : nullptr);
     }
     TL(tl_slot(tl_j, 5));
     tl_j++;
@@ -1653,7 +1663,33 @@ __global__ __launch_bounds__(kT) void decode_kernel(const uint8_t *__restrict__ 
   }
   if (pd_o) {
     store_out(pd_o, (const uint8_t *)ws.out_w, pd_lo, pd_hi, lane);
-    flush_lens(ws, pd_s, pd_m, out_len, status, lane, kGaps ? str_kind : nullptr);
+    flush_lens(ws, pd_s, pd_m, out_len, status, lane, kGaps ? str.kind : nullptr);
+  }
+  if (kGaps && str.kind) {
+    // read_strings' finish of [L0, L1) (hc/io.go:92-96), after every wave's
+    // lengths have landed: raw payloads, raw EOFs, cut regions
+    const bool clamped = bnd[2] >= str.out_cap;
+    if (clamped || fin_gate == str.gen) {  // (uniform)
+      __threadfence_block();
+      __syncthreads();
+      for (uint64_t i = L0 + tid; i < L1; i += kT) {
+        const uint8_t kd = str.kind[i];
+        if ((kd & 3u) == 2u) continue;  // ReadBit / ReadInt failed: ("", nil), as decoded
+        const uint64_t o0 = out_off[i], st0 = str.start[i], nx = str.next[i];
+        if (clamped && out_off[i + 1] - o0 < read_cap(kd, st0, str.hend[i], nx)) {
+          out_len[i] = 0;  // the region was cut short by the buffer's end
+          status[i] = (uint8_t)kStrNoSpace;
+        } else if ((kd & 3u) == 0u) {
+          const uint64_t take = nx - st0;  // next = start + take (raw)
+          if (take == 0 && (kd & kDeclared)) {
+            status[i] = (uint8_t)kStrEof;  // the block ended before the payload: io.EOF
+          } else if (take) {
+            copy_bytes(out + (o0 - out_bias), str.blk + st0, take);
+            out_len[i] = (uint32_t)take;
+          }
+        }
+      }
+    }
   }
   TL(63);
 }
@@ -1679,7 +1715,7 @@ extern "C" int mhq_diag_timeline(unsigned long long *out, int n) {
 hipError_t launch_decode(const DevTables &t, const uint8_t *in, const uint64_t *in_off, uint64_t in_bias,
                          uint64_t n, uint8_t *out, const uint64_t *out_off, uint64_t out_bias,
                          uint32_t *out_len, uint8_t *status, hipStream_t s, const uint32_t *in_end,
-                         const uint8_t *str_kind) {
+                         const StrFinish *str) {
   if (n == 0) return hipSuccess;
   // One workgroup per CU, each a contiguous range of whole wave tiles.  The
   // tile length (<= kTile) is chosen so that every wave gets the same number
@@ -1693,11 +1729,13 @@ hipError_t launch_decode(const DevTables &t, const uint8_t *in, const uint64_t *
   const uint64_t per_block = (((n + cus - 1) / cus + tl - 1) / tl) * tl;
   const unsigned grid = (unsigned)((n + per_block - 1) / per_block);
   if (in_end)
-    decode_kernel<true><<<dim3(grid), dim3(kT), 0, s>>>(in, in_off, in_end, str_kind, in_bias, n, out, out_off, out_bias,
+    decode_kernel<true><<<dim3(grid), dim3(kT), 0, s>>>(in, in_off, in_end, str ? *str : StrFinish{}, in_bias, n, out,
+                                                        out_off, out_bias,
                                                         out_len, status, t.lut1, t.lut2, t.len, per_block,
                                                         (uint32_t)tl);
   else
-    decode_kernel<false><<<dim3(grid), dim3(kT), 0, s>>>(in, in_off, nullptr, nullptr, in_bias, n, out, out_off, out_bias,
+    decode_kernel<false><<<dim3(grid), dim3(kT), 0, s>>>(in, in_off, nullptr, StrFinish{}, in_bias, n, out, out_off,
+                                                         out_bias,
                                                          out_len, status, t.lut1, t.lut2, t.len, per_block,
                                                          (uint32_t)tl);
   return hipGetLastError();

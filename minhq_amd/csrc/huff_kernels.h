@@ -39,12 +39,26 @@ hipError_t launch_encode(const DevTables &t, const uint8_t *in, const uint64_t *
 // the first position at or after in_off[i] whose low 32 bits are in_end[i]
 // (literals under 4 GiB); e_i <= in_off[i + 1] when the literals are in order
 // (any order decodes; in-order tiles are the fast ones), in_off[n] >= every
-// e_i.  str_kind (with in_end: read_strings' framed strings, kind & 3 == 1
-// for Huffman): out_len / status get ReadString's outcome (str_outcome).
+// e_i.  str (with in_end): read_strings' strings, see StrFinish.
+// read_strings' per-string data for the in_end decode (str_frame.hip): with
+// `kind`, each write of out_len / status applies ReadString's outcome
+// (str_outcome), and each workgroup ends by finishing its literal range --
+// raw payloads copied out, raw EOFs, regions cut short at out_cap -- when the
+// parse stored `gen` to *finish_needed (some string is raw) or the output is
+// cut (out_off[n] >= out_cap).
+struct StrFinish {
+  const uint8_t *kind = nullptr;
+  const uint64_t *start = nullptr, *next = nullptr;
+  const uint32_t *hend = nullptr;
+  const uint8_t *blk = nullptr;
+  uint64_t out_cap = 0;
+  const uint64_t *finish_needed = nullptr;
+  uint64_t gen = 0;
+};
 hipError_t launch_decode(const DevTables &t, const uint8_t *in, const uint64_t *in_off,
                          uint64_t in_bias, uint64_t n, uint8_t *out, const uint64_t *out_off,
                          uint64_t out_bias, uint32_t *out_len, uint8_t *status, hipStream_t s,
-                         const uint32_t *in_end = nullptr, const uint8_t *str_kind = nullptr);
+                         const uint32_t *in_end = nullptr, const StrFinish *str = nullptr);
 // out_off[i] = base + sum_{j<i} enc_len[j]; cap_off[i] = base + sum_{j<i} floor(8*enc_len[j]/5)
 // (either output may be null).  Scratch: offsets_scratch_bytes(n) bytes, or
 // null for a hipMallocAsync on `s`.

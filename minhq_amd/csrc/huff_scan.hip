@@ -2,6 +2,8 @@
 // arrays (encode output offsets and decode capacities).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include <atomic>
 
 #include "huff_common.h"
@@ -51,6 +53,9 @@ constexpr int kItems = MHQ_SCAN_ITEMS;
 static_assert(kItems % 4 == 0, "whole 16-B loads of lengths");
 constexpr int kChunk = kScanBlock * kItems;
 constexpr int kWaves = kScanBlock / kWave;
+#ifndef MHQ_SCAN_NT  // the apply pass's offsets leave as streaming stores (layout call north star 26.1 -> 24.1 us)
+#define MHQ_SCAN_NT 1
+#endif
 #ifndef MHQ_SCAN_DIRECT_U  // the apply pass's direct-sum loads in flight per thread
 #define MHQ_SCAN_DIRECT_U 16
 #endif
@@ -237,22 +242,19 @@ __global__ __launch_bounds__(kScanBlock) void scan_sums_kernel(uint64_t *sums, u
 // items) plus the superblock-local prefix of its first pair, c*g, where `g`
 // is the number of pairs per chunk: 1 for the reduce pass, kChunk /
 // kLenSumBlock for encode_len's per-block sums.
+// One chunk of the apply pass (chunk = blockIdx.x, or a chunk of a looping
+// block's share).
 template <class F>
-__global__ __launch_bounds__(kScanBlock) void scan_apply_kernel(F f, uint64_t n, const uint64_t *sums,
-                                                                 const uint64_t *sup, uint32_t g, uint64_t base,
-                                                                 uint64_t *oa, uint64_t *ob, uint64_t lim_a = ~0ull,
-                                                                 uint64_t lim_b = ~0ull,
-                                                                 const uint64_t *gate = nullptr,
-                                                                 uint64_t gen = 0) {
-  // gated (read_strings): runs only when its producer stored this call's gen
-  if (gate && __builtin_nontemporal_load(gate) != gen) return;
+__device__ __forceinline__ void scan_apply_chunk(const F &f, uint64_t n, const uint64_t *sums, const uint64_t *sup,
+                                                 uint32_t g, uint64_t base, uint64_t *oa, uint64_t *ob,
+                                                 uint64_t lim_a, uint64_t lim_b, uint64_t chunk) {
   __shared__ uint64_t sh[2 * kWaves];
   const int tid = threadIdx.x, lane = tid % kWave, wave = tid / kWave;
   // this chunk's items first: their loads are in flight during the prefix
-  const uint64_t i0 = (uint64_t)blockIdx.x * kChunk + (uint64_t)tid * kItems;
+  const uint64_t i0 = (uint64_t)chunk * kChunk + (uint64_t)tid * kItems;
   uint64_t a[kItems], b[kItems];
   f.load(i0, a, b);
-  const uint64_t first = (uint64_t)blockIdx.x * g;  // this chunk's first pair
+  const uint64_t first = (uint64_t)chunk * g;  // this chunk's first pair
   uint64_t pa = 0, pb = 0;
 #ifndef MHQ_X_SCAN  // timing experiments only (wrong output): 1 no prefix of the sums before the chunk, 2 no stores
 #define MHQ_X_SCAN 0
@@ -314,7 +316,7 @@ __global__ __launch_bounds__(kScanBlock) void scan_apply_kernel(F f, uint64_t n,
     rb += b[k];
   }
   typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
-  const uint64_t c0 = (uint64_t)blockIdx.x * kChunk;
+  const uint64_t c0 = (uint64_t)chunk * kChunk;
   if (MHQ_X_SCAN & 2) {
     if (xa[0] == 0x123456789ull) oa[0] = xb[kItems - 1];  // (keeps the values live)
   } else if (c0 + kChunk <= n + 1) {
@@ -329,8 +331,13 @@ __global__ __launch_bounds__(kScanBlock) void scan_apply_kernel(F f, uint64_t n,
     for (int k = 0; k < kItems / 2; k++) {
       const uint32_t j = 2u * ((uint32_t)tid + (uint32_t)k * kScanBlock);
       const u64x2 v0 = st[j], v1 = st[j + 1];
+#if MHQ_SCAN_NT
+      if (oa) __builtin_nontemporal_store(u64x2{v0.x, v1.x}, (u64x2 *)(oa + c0 + j));
+      if (ob) __builtin_nontemporal_store(u64x2{v0.y, v1.y}, (u64x2 *)(ob + c0 + j));
+#else
       if (oa) *(u64x2 *)(oa + c0 + j) = u64x2{v0.x, v1.x};
       if (ob) *(u64x2 *)(ob + c0 + j) = u64x2{v0.y, v1.y};
+#endif
     }
   } else if (i0 + kItems <= n + 1) {  // a whole run of outputs: 16-B stores (i0 is a multiple of 8)
 #pragma unroll
@@ -346,6 +353,35 @@ __global__ __launch_bounds__(kScanBlock) void scan_apply_kernel(F f, uint64_t n,
         if (ob) ob[i0 + k] = xb[k];
       }
     }
+  }
+}
+
+template <class F>
+__global__ __launch_bounds__(kScanBlock) void scan_apply_kernel(F f, uint64_t n, const uint64_t *sums,
+                                                                 const uint64_t *sup, uint32_t g, uint64_t base,
+                                                                 uint64_t *oa, uint64_t *ob, uint64_t lim_a = ~0ull,
+                                                                 uint64_t lim_b = ~0ull,
+                                                                 const uint64_t *gate = nullptr,
+                                                                 uint64_t gen = 0) {
+  // gated (read_strings): runs only when its producer stored this call's gen
+  if (gate && __builtin_nontemporal_load(gate) != gen) return;
+  scan_apply_chunk(f, n, sums, sup, g, base, oa, ob, lim_a, lim_b, blockIdx.x);
+}
+
+// The apply pass as a small grid looping over the chunks: for a gated pass
+// that usually does nothing (read_strings' fallback layout), a few hundred
+// workgroups that read the gate and end cost less than one per chunk.
+template <class F>
+__global__ __launch_bounds__(kScanBlock) void scan_apply_loop_kernel(F f, uint64_t n, const uint64_t *sums,
+                                                                      const uint64_t *sup, uint32_t g, uint64_t base,
+                                                                      uint64_t *oa, uint64_t *ob, uint64_t lim_a,
+                                                                      uint64_t lim_b, const uint64_t *gate,
+                                                                      uint64_t gen) {
+  if (gate && __builtin_nontemporal_load(gate) != gen) return;
+  const uint64_t nb = (n + 1 + kChunk - 1) / kChunk;
+  for (uint64_t c = blockIdx.x; c < nb; c += gridDim.x) {
+    scan_apply_chunk(f, n, sums, sup, g, base, oa, ob, lim_a, lim_b, c);
+    __syncthreads();  // the chunk's LDS is read to the end before the next one's writes
   }
 }
 
@@ -449,7 +485,8 @@ hipError_t launch_read_caps_sums(const uint64_t *start, const uint32_t *hend, co
   uint64_t *sup = block_sums + 2 * (ns + 1);
   const bool direct = direct_sums(nb, ns);
   if (!direct) scan_sums_kernel<<<dim3((unsigned)nsup), dim3(kScanBlock), 0, s>>>(block_sums, ns, sup);
-  scan_apply_kernel<ReadCapVal><<<dim3((unsigned)nb), dim3(kScanBlock), 0, s>>>(
+  // (gated, usually a no-op: a looping grid of at most 256 workgroups)
+  scan_apply_loop_kernel<ReadCapVal><<<dim3((unsigned)std::min<uint64_t>(nb, 256)), dim3(kScanBlock), 0, s>>>(
       ReadCapVal{start, next, hend, kind, n}, n, block_sums, direct ? nullptr : sup, (uint32_t)(kChunk / kLenSumBlock),
       0, out_off, nullptr, lim, lim, gate, gen);
   return hipGetLastError();

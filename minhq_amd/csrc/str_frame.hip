@@ -11,6 +11,7 @@
 // are integer/byte work with one thread per string.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <atomic>
 
 #include "huff_common.h"
@@ -18,6 +19,8 @@
 
 namespace mhq {
 namespace {
+
+using namespace dev;
 
 constexpr int kT = 256;
 
@@ -30,20 +33,12 @@ struct ReadScratch {
                     // otherwise (the decode's in_end)
   uint8_t *kind;    // 0 raw, 1 Huffman, 2 header error (hc/io.go:74-81 return ("", nil)); | kDeclared
 };
-// A string's output capacity, recomputed from its parse where it is needed
-// (the fallback layout, a cut region): floor(8*take/5) (Huffman), take (raw).
-__device__ __forceinline__ uint64_t read_cap(uint8_t kind, uint64_t start, uint32_t hend, uint64_t next) {
-  const uint32_t k = kind & 3u;
-  if (k == 1u) return (uint32_t)((uint64_t)(uint32_t)(hend - (uint32_t)start) * 8u / 5u);
-  return k == 0u ? (uint32_t)(next - start) : 0u;
-}
-constexpr uint8_t kDeclared = 4;  // the declared length is not 0
 
 // Reader.ReadBit + Reader.ReadInt(prefix) at byte pos, bit 7-prefix being the
 // H bit, reading no byte at or past limit (hc/io.go:25-55, 73-81).
 // Each block also writes the capacity sums of its strings, per kLenSumBlock,
 // to block_sums: the offsets scan's first pass.
-#ifndef MHQ_PARSE_PER  // strings per parse / finish thread: i = block * kT * kParsePer + k * kT + tid (1, 4, 8: 1-4 % slower)
+#ifndef MHQ_PARSE_PER  // strings per parse thread: i = block * kT * kParsePer + k * kT + tid (1, 4, 8: 1-4 % slower)
 #define MHQ_PARSE_PER 2
 #endif
 constexpr int kParsePer = MHQ_PARSE_PER;
@@ -138,7 +133,7 @@ __global__ __launch_bounds__(kT) void read_parse_kernel(const uint8_t *__restric
     bad |= start + take > min(pn[k], blk_len);
   }
   if (bad) *order_bad = gen;  // (rare: every writer stores the same value)
-  if (raw) *finish_needed = gen;  // raw payloads to copy: the finish pass runs
+  if (raw) *finish_needed = gen;  // raw payloads to copy: the decode finishes its ranges
   // (sum of cap, sum of cap) per kLenSumBlock strings: group k of this block
   __shared__ uint64_t part[kParsePer][kT / 64];
   const uint32_t lane = threadIdx.x % 64, wave = threadIdx.x / 64;
@@ -162,110 +157,7 @@ __global__ __launch_bounds__(kT) void read_parse_kernel(const uint8_t *__restric
   }
 }
 
-// len bytes from src to dst, any alignments, by one thread: the 0-3 bytes up
-// to dst's first dword boundary and the 0-3 after its last whole dword go as
-// bytes (neighbouring bytes untouched), the middle as dword stores of source
-// dwords realigned with v_alignbyte.  Every load of a 64-byte block is issued
-// before its first store (no load-store round trip per word).  A source dword
-// read holds at least one byte of [src, src + len): inside any 4-B aligned
-// allocation.
-__device__ __forceinline__ void copy_bytes(uint8_t *__restrict__ dst, const uint8_t *__restrict__ src,
-                                           uint64_t len) {
-  const uint32_t h = (uint32_t)min((uint64_t)((0u - (uint32_t)(uintptr_t)dst) & 3u), len);
-  const uint64_t body = (len - h) & ~(uint64_t)3;
-  const uint32_t t = (uint32_t)(len - h) & 3u;
-  uint32_t hb[3], tb[3];
-#pragma unroll
-  for (uint32_t k = 0; k < 3; k++) {
-    hb[k] = k < h ? src[k] : 0u;
-    tb[k] = k < t ? src[h + body + k] : 0u;
-  }
-  const uint8_t *s1 = src + h;
-  uint32_t *d4 = (uint32_t *)(dst + h);
-  const uint32_t r = (uint32_t)(uintptr_t)s1 & 3u;
-  const uint32_t *w = (const uint32_t *)(s1 - r);
-  const uint64_t nw = body >> 2;
-  for (uint64_t q0 = 0; q0 < nw; q0 += 16) {
-    const uint32_t nq = (uint32_t)min(nw - q0, (uint64_t)16);
-    const uint32_t nload = nq + (r != 0u);
-    uint32_t x[17];
-#pragma unroll
-    for (uint32_t j = 0; j < 17; j++) x[j] = j < nload ? w[q0 + j] : 0u;
-#pragma unroll
-    for (uint32_t j = 0; j < 16; j++)
-      if (j < nq) d4[q0 + j] = __builtin_amdgcn_alignbyte(x[j + 1], x[j], r);
-  }
-#pragma unroll
-  for (uint32_t k = 0; k < 3; k++) {
-    if (k < h) dst[k] = (uint8_t)hb[k];
-    if (k < t) dst[h + body + k] = (uint8_t)tb[k];
-  }
-}
 
-// Raw payloads into the output (after the decode), then the per-string
-// outcome of hc/io.go:92-96.  The decode has written out_len / status for
-// every string, with the Huffman strings' outcome applied (INVALID length 0,
-// EOF: str_outcome), 0 / OK for the raw and unreadable ones (empty literals
-// to it), so only raw payloads, raw EOFs and cut regions are left.  Regions
-// are cut short only at the output's end (the scan clamps the offsets to
-// out_cap), so with out_off[n] < out_cap no region is and the capacity test
-// reads nothing; with no raw string either (the parse stores `gen` to
-// *finish_needed otherwise) the pass ends at once.
-__global__ __launch_bounds__(kT) void read_finish_kernel(const uint8_t *__restrict__ blk, ReadScratch sc, uint64_t n,
-                                                         const uint64_t *__restrict__ out_off,
-                                                         const uint64_t *__restrict__ next,
-                                                         uint8_t *__restrict__ out, uint32_t *__restrict__ out_len,
-                                                         uint8_t *__restrict__ status, uint64_t out_cap,
-                                                         const uint64_t *finish_needed, uint64_t gen) {
-  const bool clamped = out_off[n] >= out_cap;  // (uniform)
-  if (!clamped && __builtin_nontemporal_load(finish_needed) != gen) return;
-  // kParsePer strings per thread as in read_parse_kernel, all loads first
-  const uint64_t i0 = (uint64_t)blockIdx.x * (kT * kParsePer) + threadIdx.x;
-  uint8_t kd[kParsePer], ds[kParsePer];
-  uint64_t o0[kParsePer], o1[kParsePer];
-  uint32_t cap[kParsePer], dl[kParsePer];
-#pragma unroll
-  for (int k = 0; k < kParsePer; k++) {
-    const uint64_t i = i0 + (uint64_t)k * kT;
-    const uint64_t j = i < n ? i : n - 1;
-    kd[k] = sc.kind[j];
-    dl[k] = out_len[j];
-    ds[k] = status[j];
-    o0[k] = o1[k] = 0;
-    cap[k] = 0;
-    if (clamped) {
-      o0[k] = out_off[j];
-      o1[k] = out_off[j + 1];
-      cap[k] = (uint32_t)read_cap(kd[k], sc.start[j], sc.hend[j], next[j]);
-    }
-  }
-#pragma unroll
-  for (int k = 0; k < kParsePer; k++) {
-    const uint64_t i = i0 + (uint64_t)k * kT;
-    if (i >= n) continue;
-    const uint8_t kind = kd[k] & 3u;
-    if (kind == 2) continue;  // ReadBit / ReadInt failed: ("", nil), as the decode left it
-    if (o1[k] - o0[k] < cap[k]) {  // the output region was cut short by the buffer's end
-      out_len[i] = 0;
-      status[i] = MHQ_STR_NOSPACE;
-    } else if (kind == 1) {
-      if (ds[k] == MHQ_LIT_INVALID) {  // ("", "invalid Huffman coding"): MHQ_STR_INVALID, length 0
-        if (dl[k] != 0) out_len[i] = 0;
-      } else if (dl[k] == 0) {
-        status[i] = MHQ_STR_EOF;  // io.ReadFull into len*8/5+1 >= 1 bytes read nothing: io.EOF
-      }
-    } else {
-      const uint64_t start = sc.start[i], take = next[i] - start;  // next = start + take (kind 0)
-      if (take == 0 && (kd[k] & kDeclared)) {
-        status[i] = MHQ_STR_EOF;  // the block ended before the payload: io.EOF
-      } else if (take) {
-        const uint64_t ob = clamped ? o0[k] : out_off[i];
-        copy_bytes(out + ob, blk + start, take);
-        out_len[i] = (uint32_t)take;
-      }
-    }
-  }
-}
 
 // ---- write side ----------------------------------------------------------
 
@@ -558,8 +450,9 @@ size_t read_strings_scratch_bytes(uint64_t n, uint64_t blk_len) { return ReadLay
 // parse (+ block sums, + the output regions at the scaled payload starts) ->
 // only if some string lies out of block order: one scan of the capacities
 // into out_off (regions back to back), clamped to the output -> decode of the
-// Huffman payloads where they lie in the block (launch_decode with in_end) ->
-// finish.  The scan's apply pass is always launched but returns at once
+// Huffman payloads where they lie in the block (launch_decode with in_end),
+// which also finishes every string (StrFinish: the Huffman outcome, raw
+// payloads, cut regions).  The scan's apply pass is always launched but returns at once
 // unless parse stored this call's generation number to order_bad (a number
 // no earlier call used: no reset, and stale scratch contents can only cause
 // the always-correct scan).
@@ -592,10 +485,22 @@ hipError_t launch_read_strings(const DevTables &t, const uint8_t *blk, uint64_t 
   // strings out of block order: capacities back to back instead
   TRY(launch_read_caps_sums(sc.start, sc.hend, next, sc.kind, n, (uint64_t *)(base + L.sums), out_cap, out_off, s,
                             order_bad, gen));
-  TRY(launch_decode(t, blk, sc.start, 0, n, out, out_off, 0, out_len, status, s, sc.hend, sc.kind));
-  read_finish_kernel<<<(unsigned)((n + kT * kParsePer - 1) / (kT * kParsePer)), kT, 0, s>>>(
-      blk, sc, n, out_off, next, out, out_len, status, out_cap, finish_needed, gen);
-  TRY(hipGetLastError());
+  {
+    // the decode also finishes each string (StrFinish): the Huffman outcome
+    // at every length it writes, then raw payloads, raw EOFs and cut regions
+    // per workgroup range when the parse flagged a raw string or the output
+    // is cut
+    StrFinish fin;
+    fin.kind = sc.kind;
+    fin.start = sc.start;
+    fin.next = next;
+    fin.hend = sc.hend;
+    fin.blk = blk;
+    fin.out_cap = out_cap;
+    fin.finish_needed = finish_needed;
+    fin.gen = gen;
+    TRY(launch_decode(t, blk, sc.start, 0, n, out, out_off, 0, out_len, status, s, sc.hend, &fin));
+  }
 done:
   if (!scratch) {
     const hipError_t e2 = hipFreeAsync(base, s);
