@@ -364,13 +364,16 @@ constexpr uint64_t kZcSlack = 64;
 // `slack` bytes after it, else null (pageable memory, hipHostRegister'ed
 // ranges whose extent the runtime does not report, buffers at a mapping's
 // very end: those go through the staged copies).
-const void *zero_copy_view(const void *p, uint64_t len, uint64_t slack = kZcSlack) {
+const void *zero_copy_view(int ordinal, const void *p, uint64_t len, uint64_t slack = kZcSlack) {
   if (!p) return nullptr;
   hipPointerAttribute_t at{};
   if (hipPointerGetAttributes(&at, p) != hipSuccess || at.type != hipMemoryTypeHost || !at.devicePointer) {
     (void)hipGetLastError();  // (pageable memory reports an error: not the caller's)
     return nullptr;
   }
+  // only memory pinned while this shard's device was current: a mapping
+  // into the other devices of a multi-device context is not assumed
+  if (at.device != ordinal) return nullptr;
   hipDeviceptr_t base = nullptr;
   size_t size = 0;
   if (hipMemGetAddressRange(&base, &size, (hipDeviceptr_t)p) != hipSuccess || !base) {
@@ -391,24 +394,24 @@ bool run_zero_copy(Device *d, const HostJob &j, uint64_t a, uint64_t b, int &rc)
   if (!MHQ_HOST_ZERO_COPY) return false;
   const uint64_t m = b - a;
   const uint64_t n_all_in = j.in_off[b] - j.in_off[0];  // the view must reach the shard's end
-  const uint8_t *din = (const uint8_t *)zero_copy_view(j.in, n_all_in ? n_all_in : 1);
-  const uint64_t *din_off = (const uint64_t *)zero_copy_view(j.in_off + a, (m + 1) * sizeof(uint64_t));
+  const uint8_t *din = (const uint8_t *)zero_copy_view(d->ordinal, j.in, n_all_in ? n_all_in : 1);
+  const uint64_t *din_off = (const uint64_t *)zero_copy_view(d->ordinal, j.in_off + a, (m + 1) * sizeof(uint64_t));
   if (!din || !din_off) return false;
   hipStream_t s = d->st[0].s;
   if (j.op == Op::kEncodeLen) {
-    uint32_t *dl = (uint32_t *)zero_copy_view(j.lens + a, m * sizeof(uint32_t), 0);
+    uint32_t *dl = (uint32_t *)zero_copy_view(d->ordinal, j.lens + a, m * sizeof(uint32_t), 0);
     if (!dl) return false;
     rc = hip_rc(mhq::launch_encode_len(d->tables, din, din_off, j.in_off[0], m, dl, s));
   } else {
     const uint64_t n_all_out = j.out_off[b] - j.out_off[0];
-    uint8_t *dout = (uint8_t *)zero_copy_view(j.out, n_all_out ? n_all_out : 1, 0);
-    const uint64_t *dout_off = (const uint64_t *)zero_copy_view(j.out_off + a, (m + 1) * sizeof(uint64_t));
+    uint8_t *dout = (uint8_t *)zero_copy_view(d->ordinal, j.out, n_all_out ? n_all_out : 1, 0);
+    const uint64_t *dout_off = (const uint64_t *)zero_copy_view(d->ordinal, j.out_off + a, (m + 1) * sizeof(uint64_t));
     if (!dout || !dout_off) return false;
     if (j.op == Op::kEncode) {
       rc = hip_rc(mhq::launch_encode(d->tables, din, din_off, j.in_off[0], m, dout, dout_off, j.out_off[0], s));
     } else {
-      uint32_t *dl = (uint32_t *)zero_copy_view(j.lens + a, m * sizeof(uint32_t), 0);
-      uint8_t *dst = (uint8_t *)zero_copy_view(j.status + a, m, 0);
+      uint32_t *dl = (uint32_t *)zero_copy_view(d->ordinal, j.lens + a, m * sizeof(uint32_t), 0);
+      uint8_t *dst = (uint8_t *)zero_copy_view(d->ordinal, j.status + a, m, 0);
       if (!dl || !dst) return false;
       rc = hip_rc(mhq::launch_decode(d->tables, din, din_off, j.in_off[0], m, dout, dout_off, j.out_off[0], dl, dst,
                                      s));

@@ -13,7 +13,7 @@ static void show(const char *what, void *p) {
   hipDeviceptr_t base = nullptr;
   size_t size = 0;
   const hipError_t e2 = hipMemGetAddressRange(&base, &size, (hipDeviceptr_t)p);
-  printf("%-22s attr=%d type=%d host=%p dev=%p (p=%p) range=%d base=%p size=%zu\n", what, (int)e, (int)a.type,
+  printf("%-22s attr=%d type=%d device=%d host=%p dev=%p (p=%p) range=%d base=%p size=%zu\n", what, (int)e, (int)a.type, a.device,
          a.hostPointer, a.devicePointer, p, (int)e2, base, size);
   (void)hipGetLastError();
 }
