@@ -186,6 +186,9 @@ inline unsigned tile_grid(uint64_t ntiles, int waves, int per_cu) {
 // kind: 0 raw, 1 Huffman, 2 header error (hc/io.go:74-81 return ("", nil)),
 // | kDeclared when the declared length is not 0.
 constexpr uint8_t kDeclared = 4;
+// A framed string's output region in the positional layout: floor(8 x / 5)
+// of its payload start x, without overflow (str_frame.hip).
+__device__ __forceinline__ uint64_t region_at(uint64_t x) { return x / 5u * 8u + (x % 5u) * 8u / 5u; }
 // A string's output capacity, recomputed from its parse where it is needed
 // (the fallback layout, a cut region): floor(8*take/5) (Huffman), take (raw).
 __device__ __forceinline__ uint64_t read_cap(uint8_t kind, uint64_t start, uint32_t hend, uint64_t next) {

@@ -59,6 +59,29 @@ hipError_t launch_decode(const DevTables &t, const uint8_t *in, const uint64_t *
                          uint64_t in_bias, uint64_t n, uint8_t *out, const uint64_t *out_off,
                          uint64_t out_bias, uint32_t *out_len, uint8_t *status, hipStream_t s,
                          const uint32_t *in_end = nullptr, const StrFinish *str = nullptr);
+// read_strings in one pass (str_frame.hip, MHQ_RS_FUSED): the frames parsed
+// from each staged tile, decoded in place, raw payloads copied, every output
+// written; strings out of block order (or a header past the next string's
+// pos) store gen to *fallback, and the caller then runs the multi-pass
+// pipeline gated on it.  sc_*: the parse of tiles too long to stage (read by
+// their streamed decode).
+hipError_t launch_read_fused(const DevTables &t, const uint8_t *blk, uint64_t blk_len, const uint64_t *pos,
+                             const uint64_t *limit, const uint8_t *prefix, uint64_t n, uint8_t *out,
+                             uint64_t *out_off, uint32_t *out_len, uint8_t *status, uint64_t *next,
+                             uint64_t *sc_start, uint32_t *sc_hend, uint8_t *sc_kind, uint64_t *fallback,
+                             uint64_t *bar, uint64_t gen, hipStream_t s);
+// The fallback of launch_read_fused, one launch that returns at
+// once unless *fallback == gen: parse, the scan (strings out of order) and
+// the decode of the multi-pass pipeline as phases between grid barriers.
+// bar: one word, zeroed by launch_read_fused's kernel; wg_sums:
+// kReadFallbackMaxWgs words.
+constexpr unsigned kReadFallbackMaxWgs = 1024;
+hipError_t launch_read_fallback(const DevTables &t, const uint8_t *blk, uint64_t blk_len, const uint64_t *pos,
+                                const uint64_t *limit, const uint8_t *prefix, uint64_t n, uint8_t *out,
+                                uint64_t out_cap, uint64_t *out_off, uint32_t *out_len, uint8_t *status,
+                                uint64_t *next, uint64_t *sc_start, uint32_t *sc_hend, uint8_t *sc_kind,
+                                uint64_t *fallback, uint64_t *order_bad, uint64_t *finish_needed, uint64_t *bar,
+                                uint64_t *wg_sums, uint64_t gen, hipStream_t s);
 // out_off[i] = base + sum_{j<i} enc_len[j]; cap_off[i] = base + sum_{j<i} floor(8*enc_len[j]/5)
 // (either output may be null).  Scratch: offsets_scratch_bytes(n) bytes, or
 // null for a hipMallocAsync on `s`.

@@ -426,7 +426,7 @@ namespace {
 
 // read_strings' scratch, 16-B aligned pieces of one allocation.
 struct ReadLayout {
-  size_t start, hend, kind, flags, sums, total;
+  size_t start, hend, kind, flags, sums, coop, total;
   ReadLayout(uint64_t n, uint64_t blk_len) {
     size_t o = 0;
     auto take_ = [&](size_t bytes) {
@@ -437,13 +437,19 @@ struct ReadLayout {
     start = take_(8 * (n + 1));
     hend = take_(4 * n);
     kind = take_(n);
-    flags = take_(16);  // order_bad, finish_needed
+    flags = take_(24);  // order_bad, finish_needed, fallback (the fused pass)
     sums = take_(offsets_sums_scratch_bytes(n));
+    coop = take_(8 * (1 + kReadFallbackMaxWgs));  // the fused read's fallback: barrier word, workgroup sums
     total = o;
   }
 };
 
 }  // namespace
+
+#ifndef MHQ_RS_FUSED  // read_strings: 1 the one-pass kernel, the multi-pass pipeline as its fallback
+#define MHQ_RS_FUSED 0
+#endif
+constexpr bool kFused = MHQ_RS_FUSED;
 
 size_t read_strings_scratch_bytes(uint64_t n, uint64_t blk_len) { return ReadLayout(n, blk_len).total; }
 
@@ -468,7 +474,7 @@ hipError_t launch_read_strings(const DevTables &t, const uint8_t *blk, uint64_t 
   hipError_t e = hipSuccess;
   if (!base && (e = hipMallocAsync((void **)&base, L.total, s)) != hipSuccess) return e;
   ReadScratch sc{(uint64_t *)(base + L.start), (uint32_t *)(base + L.hend), base + L.kind};
-  uint64_t *order_bad = (uint64_t *)(base + L.flags), *finish_needed = order_bad + 1;
+  uint64_t *order_bad = (uint64_t *)(base + L.flags), *finish_needed = order_bad + 1, *fallback = order_bad + 2;
   // (one generation number per call: the flags are set by storing it, never
   // cleared, so a stale scratch cannot gate this call's passes)
   static std::atomic<uint64_t> g_gen{0};
@@ -478,6 +484,18 @@ hipError_t launch_read_strings(const DevTables &t, const uint8_t *blk, uint64_t 
     e = (x);                     \
     if (e != hipSuccess) goto done; \
   } while (0)
+  // MHQ_RS_FUSED: one pass (launch_read_fused), then its fallback, one
+  // launch that returns at once unless the pass stored gen to *fallback
+  if (kFused) {
+    uint64_t *coop = (uint64_t *)(base + L.coop);
+    TRY(launch_read_fused(t, blk, blk_len, pos, limit, prefix, n, out, out_off, out_len, status, next, sc.start,
+                          sc.hend, sc.kind, fallback, coop, gen, s));
+#ifndef MHQ_X_NOFB  // timing experiment only (no fallback: wrong for strings out of order)
+    TRY(launch_read_fallback(t, blk, blk_len, pos, limit, prefix, n, out, out_cap, out_off, out_len, status, next,
+                             sc.start, sc.hend, sc.kind, fallback, order_bad, finish_needed, coop, coop + 1, gen, s));
+#endif
+    goto done;
+  }
   read_parse_kernel<<<(unsigned)((n + kT * kParsePer - 1) / (kT * kParsePer)), kT, 0, s>>>(
       blk, blk_len, pos, limit, prefix, n, sc, next, (uint64_t *)(base + L.sums), out_off, order_bad, finish_needed,
       gen);

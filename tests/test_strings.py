@@ -226,6 +226,45 @@ def test_read_gaps_full_tiles(codec, oracle_mod):
     assert (np.asarray(st) == OK).all()
 
 
+def test_read_full_tiles_long_and_raw(codec, oracle_mod):
+    """Full tiles in block order where some tiles hold long strings (too many
+    bytes to stage: they stream, their frames parsed from global memory) and
+    raw strings in both kinds of tile (payloads copied by the read itself);
+    every long or raw string and a sample of the rest against the oracle, every
+    status and next."""
+    import numpy as np
+
+    rng = random.Random(35)
+    alpha = b"abcdefghijklmnopqrstuvwxyz0123456789-_./:;=, "
+    n = 1 << 18
+    blk, pos, special = bytearray(), [], []
+    short = [oracle_mod.write_string(bytes(rng.choice(alpha) for _ in range(rng.randint(0, 40))), prefix=7,
+                                     choice=rng.choice([1, 1, 1, 2, 0])) for _ in range(4096)]
+    for k in range(n):
+        pos.append(len(blk))
+        r = rng.random()
+        if r < 0.004:  # a long string: its tile streams
+            s = bytes(rng.choice(alpha) for _ in range(rng.randint(300, 3000)))
+            blk += oracle_mod.write_string(s, prefix=7, choice=rng.choice([1, 2]))
+            special.append(k)
+        elif r < 0.02:  # raw, maybe binary
+            s = bytes(rng.randrange(256) for _ in range(rng.randint(0, 50)))
+            blk += oracle_mod.write_string(s, prefix=7, choice=2)
+            special.append(k)
+        else:
+            blk += short[rng.randrange(len(short))]
+    blk = bytes(blk)
+    vals, st, nxt = codec.read_strings(blk, pos, [7] * n)
+    check = sorted(set(special) | set(rng.sample(range(n), 20000)))
+    for i in check:
+        end = pos[i + 1] if i + 1 < n else len(blk)
+        ref, rc, used = oracle_mod.read_string(blk[pos[i]:end], prefix=7)
+        assert (vals[i], int(st[i])) == (ref, _oracle_status(rc)), i
+        assert int(nxt[i]) == pos[i] + used, i
+    assert (np.asarray(nxt, dtype=np.uint64) == np.asarray(pos[1:] + [len(blk)], dtype=np.uint64)).all()
+    assert int((np.asarray(st) == EOF).sum()) == sum(1 for i in range(n) if blk[pos[i]] in (0x80,))
+
+
 def test_read_wild_pos_and_reverse_order_at_buffer_end(codec, oracle_mod):
     """strings read in reverse block order and header-error
     strings whose pos lies far past the block, with the block ending exactly
