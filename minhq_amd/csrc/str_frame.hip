@@ -447,7 +447,7 @@ struct ReadLayout {
 }  // namespace
 
 #ifndef MHQ_RS_FUSED  // read_strings: 1 the one-pass kernel, the multi-pass pipeline as its fallback
-#define MHQ_RS_FUSED 0
+#define MHQ_RS_FUSED 1
 #endif
 constexpr bool kFused = MHQ_RS_FUSED;
 
