@@ -2064,6 +2064,9 @@ struct RsFallback {
 __device__ void grid_barrier(uint64_t *w, uint32_t want) {
   __syncthreads();
   if (threadIdx.x == 0) {
+    // (the two device-scope fences -- L2 write-back before, invalidate after
+    // -- are most of the barrier's cost: 20 us of the shuffled block's 76
+    // with two barriers, profiles/r04c_read_fallback_fences.txt)
     __threadfence();
     unsigned long long *ww = (unsigned long long *)w;
     atomicAdd(ww, 1ull);
