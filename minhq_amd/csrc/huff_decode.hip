@@ -2060,8 +2060,11 @@ struct RsFallback {
 };
 
 // Every workgroup arrives (a.bar: zeroed by read_fused_kernel, ahead in the
-// stream); returns when `want` have.
-__device__ void grid_barrier(uint64_t *w, uint32_t want) {
+// stream); returns true when `want` have, false after 2 s without (the grid
+// not resident together: a CU mask, say) -- a safety net, never a hang.
+constexpr uint64_t kBarrierTimeout = 200000000ull;  // s_memrealtime ticks (100 MHz)
+__device__ bool grid_barrier(uint64_t *w, uint32_t want) {
+  __shared__ uint32_t ok_s;
   __syncthreads();
   if (threadIdx.x == 0) {
     // (the two device-scope fences -- L2 write-back before, invalidate after
@@ -2071,10 +2074,28 @@ __device__ void grid_barrier(uint64_t *w, uint32_t want) {
     unsigned long long *ww = (unsigned long long *)w;
     atomicAdd(ww, 1ull);
     // (relaxed polls: an acquire per poll would invalidate the L2 each time)
-    while (__hip_atomic_load(ww, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want) __builtin_amdgcn_s_sleep(2);
+    const uint64_t t0 = wall_clock64();
+    uint32_t ok = 1;
+    while (__hip_atomic_load(ww, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want) {
+      __builtin_amdgcn_s_sleep(2);
+      if (wall_clock64() - t0 > kBarrierTimeout) {
+        ok = 0;
+        break;
+      }
+    }
     __threadfence();
+    ok_s = ok;
   }
   __syncthreads();
+  return ok_s != 0;
+}
+
+constexpr uint8_t kStrIncomplete = 4;  // MHQ_STR_INCOMPLETE
+__device__ void mark_incomplete(const RsArgs &a, uint64_t L0, uint64_t L1) {
+  for (uint64_t i = L0 + threadIdx.x; i < L1; i += kT) {
+    a.out_len[i] = 0;
+    a.status[i] = kStrIncomplete;
+  }
 }
 
 // Sum of v over the workgroup (every thread gets it); red: kWaves words.
@@ -2126,7 +2147,7 @@ __global__ __launch_bounds__(kT) void read_fallback_kernel(RsFallback f, const u
   if (raw) *f.finish_needed = a.gen;
   const uint64_t total = wg_sum(csum, red);
   if (tid == 0) f.wg_sums[blockIdx.x] = total;
-  grid_barrier(a.bar, nwg);
+  if (!grid_barrier(a.bar, nwg)) return mark_incomplete(a, L0, L1);
   if (__builtin_nontemporal_load(f.order_bad) == a.gen) {  // (the whole grid alike)
     // out of block order: the capacities back to back, clamped to out_cap
     uint64_t base = 0;
@@ -2154,7 +2175,7 @@ __global__ __launch_bounds__(kT) void read_fallback_kernel(RsFallback f, const u
       base += all;
     }
     if (L1 == n && tid == 0) a.out_off[n] = min(base, f.out_cap);
-    grid_barrier(a.bar, 2u * nwg);
+    if (!grid_barrier(a.bar, 2u * nwg)) return mark_incomplete(a, L0, L1);
   }
   StrFinish str;
   str.kind = a.sc_kind;

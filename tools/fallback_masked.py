@@ -1,0 +1,62 @@
+#!/usr/bin/env python3
+"""read_strings' out-of-order fallback when its grid cannot be resident at once.
+
+Run with the process's queues limited to a few CUs (HSA_CU_MASK) so that the
+fallback kernel's grid barriers cannot complete: the call must still return
+(each barrier gives up after 2 s) with MHQ_STR_INCOMPLETE for the strings of
+the workgroups that gave up, never hang.  Without a mask every status is an
+ordinary ReadString outcome.  Prints one JSON line.
+
+    HSA_CU_MASK=0:0-31 python3 tools/fallback_masked.py
+"""
+import json
+import os
+import random
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from minhq_amd import _lib, hc  # noqa: E402
+from oracle import oracle  # noqa: E402
+
+
+def main():
+    rng = random.Random(5)
+    alpha = b"abcdefghijklmnopqrstuvwxyz0123456789-_./:;=, "
+    n = 1 << 16
+    frames = [oracle.write_string(bytes(rng.choice(alpha) for _ in range(rng.randint(1, 40))), prefix=7, choice=1)
+              for _ in range(n)]
+    pos = np.zeros(n, dtype=np.uint64)
+    pos[1:] = np.cumsum([len(f) for f in frames])[:-1]
+    blk = b"".join(frames)
+    P = pos[::-1].copy()  # reverse block order: the fused pass sends the call to the fallback
+    dev = torch.device("cuda:0")
+    codec = hc.Codec(devices=[0])
+    t_blk = torch.frombuffer(bytearray(blk), dtype=torch.uint8).to(dev)
+    t_pos = torch.from_numpy(P.view(np.int64)).to(dev)
+    t_lim = torch.full((n,), len(blk), dtype=torch.int64, device=dev)
+    t_pf = torch.full((n,), 7, dtype=torch.uint8, device=dev)
+    out = torch.zeros(len(blk) * 8 // 5 + 16, dtype=torch.uint8, device=dev)
+    out_off = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+    out_len = torch.zeros(n, dtype=torch.int32, device=dev)
+    st = torch.zeros(n, dtype=torch.uint8, device=dev)
+    nxt = torch.zeros(n, dtype=torch.int64, device=dev)
+    t0 = time.perf_counter()
+    codec.read_strings_dev(t_blk, t_pos, t_lim, t_pf, out, out_off, out_len, st, nxt)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    s = st.cpu().numpy()
+    counts = {int(k): int(v) for k, v in zip(*np.unique(s, return_counts=True))}
+    ok = int(counts.get(_lib.MHQ_STR_OK, 0))
+    print(json.dumps({"cu_mask": os.environ.get("HSA_CU_MASK", ""), "strings": n, "seconds": round(dt, 3),
+                      "status_counts": counts, "ok": ok,
+                      "incomplete": int(counts.get(_lib.MHQ_STR_INCOMPLETE, 0))}), flush=True)
+    codec.close()
+
+
+if __name__ == "__main__":
+    main()
