@@ -140,9 +140,6 @@ int mhq_huff_decode_dev(mhq_ctx *ctx, int dev, const uint8_t *in, const uint64_t
 #define MHQ_STR_INVALID 1 /* ("", "invalid Huffman coding") */
 #define MHQ_STR_EOF 2     /* ("", io.EOF): nothing decoded from a Huffman literal, or a raw one cut to 0 bytes */
 #define MHQ_STR_NOSPACE 3 /* the output buffer could not hold this string (not a reference outcome) */
-#define MHQ_STR_INCOMPLETE 4 /* not read: the device could not run the call's out-of-order pass (its
-                              * workgroups were not resident together within 2 s, e.g. under a CU mask);
-                              * not a reference outcome */
 
 /* HuffmanCodingChoice (hc/io.go:140-150). */
 #define MHQ_HUFF_AUTO 0   /* Huffman iff strictly shorter (hc/io.go:172) */

@@ -23,7 +23,6 @@ MHQ_STR_OK = 0
 MHQ_STR_INVALID = 1
 MHQ_STR_EOF = 2
 MHQ_STR_NOSPACE = 3
-MHQ_STR_INCOMPLETE = 4
 MHQ_INT_OK = 0
 MHQ_INT_EOF = 1
 MHQ_INT_OVERFLOW = 2

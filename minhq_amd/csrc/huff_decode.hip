@@ -1491,7 +1491,10 @@ __device__ __forceinline__ void decode_body(Smem &sm, const uint8_t *__restrict_
   // then its output offsets, the tables and the second tile's offsets.
   // (Every wave loads them, as scalar loads, and waits for them only where
   // they are used: a load under `tid == 0` waited at once.)
-  const uint64_t bnd[4] = {in_off[n], in_off[0], out_off[n], out_off[0]};
+  const bool local = kGaps && str.local;  // (uniform)
+  const uint64_t bnd[4] = {in_off[local ? L1 : n], in_off[local ? L0 : 0], out_off[local ? L1 : n],
+                           out_off[local ? L0 : 0]};
+  const uint64_t nb = local ? L1 - L0 : n;
   // read_strings: whether this workgroup finishes its range at the end (its
   // gate word loaded now, used there)
   const uint64_t fin_gate = kGaps && str.finish_needed ? __builtin_nontemporal_load(str.finish_needed) : 0;
@@ -1535,7 +1538,7 @@ __device__ __forceinline__ void decode_body(Smem &sm, const uint8_t *__restrict_
   // every lane a literal (longer literals keep tl0 and stream).
   if (tid == 0) {
     const uint64_t nin = bnd[0] - bnd[1], nout = bnd[2] - bnd[3];
-    const uint64_t ain = (nin + n - 1) / n, aout = (nout + n - 1) / n;
+    const uint64_t ain = (nin + nb - 1) / nb, aout = (nout + nb - 1) / nb;
     // kGaps (read_strings): a 20 % margin, not 25: its means include the
     // frame headers and the scaled regions' slack (config 2: 27.5 and 44 B
     // against 26.5 and 42.4), and a tile length cut below tl0 gives some
@@ -1743,7 +1746,6 @@ struct RsArgs {
   uint8_t *sc_kind;
   uint64_t *fallback;
   uint64_t gen;
-  uint64_t *bar;  // the fallback's barrier count, zeroed here
 };
 
 struct RsTile {  // pos / limit / prefix of strings s + 2 lane + {0, 1}; pos of string s + tile
@@ -1848,7 +1850,6 @@ __global__ __launch_bounds__(kT) void read_fused_kernel(RsArgs a, const uint32_t
   const uint32_t lane = tid % kWave;
   const uint32_t wave = tid / kWave;
   const uint64_t L0 = (uint64_t)blockIdx.x * per_block;
-  if (tid == 0 && blockIdx.x == 0) *a.bar = 0;  // (read_fallback_kernel's barriers count from 0)
   if (L0 >= a.n) return;
   const uint64_t L1 = min(L0 + per_block, a.n);
   WaveSmem &ws = sm.w[wave];
@@ -1943,10 +1944,12 @@ __global__ __launch_bounds__(kT) void read_fused_kernel(RsArgs a, const uint32_t
         const uint64_t lim = min(h ? rt.l1 : rt.l0, blk_len);
         const uint32_t pf = (rt.pf >> (8 * h)) & 0xffu;
         const uint64_t pn = j + 1u < cnt ? (h ? nx : rt.p1) : pe;  // the next string's pos (order test)
-        const RsStr r = rs_parse(p, lim, pf, blk_len, lo, hi, [&](uint64_t q) -> uint32_t {
+        RsStr r = rs_parse(p, lim, pf, blk_len, lo, hi, [&](uint64_t q) -> uint32_t {
           return fits ? slice_byte(ws, (uint32_t)(q - ps) + idelta) : (uint32_t)a.blk[q];
         });
-        bad |= r.far || r.start + r.take > min(pn, blk_len);
+        if (r.far)  // a header octet outside the staged span: from global memory (bad below unless it failed)
+          r = rs_parse(p, lim, pf, blk_len, 0, blk_len, [&](uint64_t q) -> uint32_t { return a.blk[q]; });
+        bad |= r.start + r.take > min(pn, blk_len);  // read_parse_kernel's order test
         const uint32_t k = r.kind & 3u;
         const uint64_t hend = k == 1u ? r.start + r.take : r.start;
         const uint64_t reg = region_at(r.start), i = s + j;
@@ -2038,65 +2041,30 @@ __global__ __launch_bounds__(kT) void read_fused_kernel(RsArgs a, const uint32_t
   }
 }
 
-// ---- the fused read's fallback: the multi-pass read in one gated launch ---
-// When read_fused_kernel stored gen to *fallback (strings out of block order,
-// or a header past the next string's pos), this kernel redoes the whole call
-// as read_parse_kernel -> the capacities scan -> decode_kernel<true> would
-// (str_frame.hip), as three phases of one launch between grid barriers: the
-// parse of each workgroup's decode range (+ its capacity sum), if some string
-// is out of order the regions laid out back to back (clamped to out_cap), then
-// the decode with its finish.  Otherwise every workgroup returns at once: one
-// launch instead of three gated ones (6.4 us of the call on the config-2
-// block).  The grid is at most one workgroup per CU, the most the decode's
-// LDS allows, so its workgroups are resident together once the stream's
-// previous kernel is done (other streams' kernels only delay some until
-// theirs end); a cooperative launch, which guarantees it, cost 60-100 us a
-// call here.
+// ---- the fused read's fallback: strings out of block order, one launch ----
+// When read_fused_kernel stored gen to *fallback (some string's payload runs
+// past the next string's pos: the strings are out of block order), this
+// kernel redoes the call as read_parse_kernel -> the capacities scan ->
+// decode_kernel<true> would (str_frame.hip) for out-of-order strings: regions
+// back to back, clamped to out_cap.  Each workgroup parses its decode range
+// (and the string after it, whose payload start bounds its last tile),
+// publishes its capacity sum, adds up its predecessors' sums as they appear
+// (decoupled look-back: every predecessor publishes right after its own
+// parse, so one round usually sees them all), lays out its regions and
+// decodes its range with the range's own bounds (StrFinish::local).  No
+// workgroup reads another's data except the published sums (agent-scope
+// atomics): no grid barrier, no device-wide fence, and a workgroup only ever
+// waits for lower-numbered ones, which the dispatcher started first -- no
+// assumption that the grid is resident at once.  In block order every
+// workgroup returns at once: one launch instead of three gated ones (6.4 us
+// of the call on the config-2 block).
 struct RsFallback {
   RsArgs a;
   uint64_t out_cap;
-  uint64_t *order_bad, *finish_needed;
-  uint64_t *wg_sums;  // capacity sum per workgroup
+  uint64_t *wg_agg;  // per workgroup: gen's low 24 bits << 40 | capacity sum
+  uint64_t *wg_fin;  // per workgroup: gen when its range holds a raw string
 };
-
-// Every workgroup arrives (a.bar: zeroed by read_fused_kernel, ahead in the
-// stream); returns true when `want` have, false after 2 s without (the grid
-// not resident together: a CU mask, say) -- a safety net, never a hang.
-constexpr uint64_t kBarrierTimeout = 200000000ull;  // s_memrealtime ticks (100 MHz)
-__device__ bool grid_barrier(uint64_t *w, uint32_t want) {
-  __shared__ uint32_t ok_s;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    // (the two device-scope fences -- L2 write-back before, invalidate after
-    // -- are most of the barrier's cost: 20 us of the shuffled block's 76
-    // with two barriers, profiles/r04c_read_fallback_fences.txt)
-    __threadfence();
-    unsigned long long *ww = (unsigned long long *)w;
-    atomicAdd(ww, 1ull);
-    // (relaxed polls: an acquire per poll would invalidate the L2 each time)
-    const uint64_t t0 = wall_clock64();
-    uint32_t ok = 1;
-    while (__hip_atomic_load(ww, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want) {
-      __builtin_amdgcn_s_sleep(2);
-      if (wall_clock64() - t0 > kBarrierTimeout) {
-        ok = 0;
-        break;
-      }
-    }
-    __threadfence();
-    ok_s = ok;
-  }
-  __syncthreads();
-  return ok_s != 0;
-}
-
-constexpr uint8_t kStrIncomplete = 4;  // MHQ_STR_INCOMPLETE
-__device__ void mark_incomplete(const RsArgs &a, uint64_t L0, uint64_t L1) {
-  for (uint64_t i = L0 + threadIdx.x; i < L1; i += kT) {
-    a.out_len[i] = 0;
-    a.status[i] = kStrIncomplete;
-  }
-}
+constexpr uint64_t kAggBits = 40;  // a workgroup's capacity sum < 2^40
 
 // Sum of v over the workgroup (every thread gets it); red: kWaves words.
 __device__ __forceinline__ uint64_t wg_sum(uint64_t v, uint64_t *red) {
@@ -2119,64 +2087,77 @@ __global__ __launch_bounds__(kT) void read_fallback_kernel(RsFallback f, const u
   __shared__ uint64_t red[kWaves];
   const RsArgs &a = f.a;
   if (__builtin_nontemporal_load(a.fallback) != a.gen) return;  // (the whole grid alike)
-  const uint32_t tid = threadIdx.x, nwg = gridDim.x;
+  const uint32_t tid = threadIdx.x, b = blockIdx.x;
   const uint64_t n = a.n, blk_len = a.blk_len;
-  const uint64_t L0 = (uint64_t)blockIdx.x * per_block, L1 = min(L0 + per_block, n);
-  // parse (read_parse_kernel's rules, str_frame.hip)
+  const uint64_t L0 = (uint64_t)b * per_block, L1 = min(L0 + per_block, n);
+  const uint64_t tag = (a.gen & 0xffffffull) << kAggBits;
+  // parse (read_parse_kernel's rules, str_frame.hip) of [L0, L1] -- string L1
+  // too (its payload start is in_off[L1], read by this range's last tile; its
+  // own workgroup writes the same value)
   uint64_t csum = 0;
-  bool bad = false, raw = false;
-  for (uint64_t i = L0 + tid; i < L1; i += kT) {
-    const uint64_t p = a.pos[i], pn = i + 1 < n ? a.pos[i + 1] : blk_len;
-    const RsStr r = rs_parse(p, min(a.limit[i], blk_len), a.prefix[i], blk_len, 0, blk_len,
+  bool raw = false;
+  for (uint64_t i = L0 + tid; i <= L1; i += kT) {
+    if (i == n) {
+      a.sc_start[n] = blk_len;
+      break;
+    }
+    const RsStr r = rs_parse(a.pos[i], min(a.limit[i], blk_len), a.prefix[i], blk_len, 0, blk_len,
                              [&](uint64_t q) -> uint32_t { return a.blk[q]; });
-    const uint32_t k = r.kind & 3u;
     a.sc_start[i] = r.start;
+    if (i == L1) break;
+    const uint32_t k = r.kind & 3u;
     a.sc_hend[i] = (uint32_t)(k == 1u ? r.start + r.take : r.start);
     a.sc_kind[i] = (uint8_t)r.kind;
-    a.next[i] = k == 2u ? p : r.start + r.take;
-    a.out_off[i] = region_at(r.start);
-    if (i == n - 1) {
-      a.sc_start[n] = blk_len;
-      a.out_off[n] = region_at(blk_len);
-    }
+    a.next[i] = k == 2u ? a.pos[i] : r.start + r.take;
     csum += k == 1u ? r.take * 8u / 5u : (k == 0u ? r.take : 0u);
     raw |= k == 0u;
-    bad |= r.start + r.take > min(pn, blk_len);
   }
-  if (bad) *f.order_bad = a.gen;  // (every writer stores the same value)
-  if (raw) *f.finish_needed = a.gen;
+  const bool any_raw = __syncthreads_or(raw);
+  if (tid == 0) f.wg_fin[b] = any_raw ? a.gen : 0u;
   const uint64_t total = wg_sum(csum, red);
-  if (tid == 0) f.wg_sums[blockIdx.x] = total;
-  if (!grid_barrier(a.bar, nwg)) return mark_incomplete(a, L0, L1);
-  if (__builtin_nontemporal_load(f.order_bad) == a.gen) {  // (the whole grid alike)
-    // out of block order: the capacities back to back, clamped to out_cap
-    uint64_t base = 0;
-    for (uint32_t g = tid; g < blockIdx.x; g += kT) base += f.wg_sums[g];
-    base = wg_sum(base, red);
-    for (uint64_t c0 = L0; c0 < L1; c0 += kT) {
-      const uint64_t i = c0 + tid;
-      const uint64_t cap = i < L1 ? read_cap(a.sc_kind[i], a.sc_start[i], a.sc_hend[i], a.next[i]) : 0u;
-      uint64_t x = cap;  // inclusive scan over the wave, then over the waves
-#pragma unroll
-      for (int d = 1; d < kWave; d <<= 1) {
-        const uint64_t y = __shfl_up((unsigned long long)x, d);
-        if ((tid % kWave) >= (uint32_t)d) x += y;
+  if (tid == 0) __hip_atomic_store((unsigned long long *)f.wg_agg + b, tag | total, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+  // look-back: the sums of workgroups 0 .. b-1, each once it carries this
+  // call's tag (every thread takes every kT-th predecessor)
+  uint64_t base = 0;
+  for (uint32_t g0 = 0; g0 < b; g0 += kT) {
+    const uint32_t g = g0 + tid;
+    uint64_t v = 0;
+    if (g < b) {
+      for (;;) {
+        v = __hip_atomic_load((unsigned long long *)f.wg_agg + g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if ((v & ~((1ull << kAggBits) - 1u)) == tag) break;
+        __builtin_amdgcn_s_sleep(1);
       }
-      if (tid % kWave == kWave - 1) red[tid / kWave] = x;
-      __syncthreads();
-      uint64_t before = 0, all = 0;
-#pragma unroll
-      for (int w = 0; w < kWaves; w++) {
-        before += w < (int)(tid / kWave) ? red[w] : 0u;
-        all += red[w];
-      }
-      __syncthreads();
-      if (i < L1) a.out_off[i] = min(base + before + x - cap, f.out_cap);
-      base += all;
     }
-    if (L1 == n && tid == 0) a.out_off[n] = min(base, f.out_cap);
-    if (!grid_barrier(a.bar, 2u * nwg)) return mark_incomplete(a, L0, L1);
+    base += v & ((1ull << kAggBits) - 1u);
   }
+  base = wg_sum(base, red);
+  // the regions back to back from base, clamped to out_cap
+  for (uint64_t c0 = L0; c0 < L1; c0 += kT) {
+    const uint64_t i = c0 + tid;
+    const uint64_t cap = i < L1 ? read_cap(a.sc_kind[i], a.sc_start[i], a.sc_hend[i], a.next[i]) : 0u;
+    uint64_t x = cap;  // inclusive scan over the wave, then over the waves
+#pragma unroll
+    for (int d = 1; d < kWave; d <<= 1) {
+      const uint64_t y = __shfl_up((unsigned long long)x, d);
+      if ((tid % kWave) >= (uint32_t)d) x += y;
+    }
+    if (tid % kWave == kWave - 1) red[tid / kWave] = x;
+    __syncthreads();
+    uint64_t before = 0, all = 0;
+#pragma unroll
+    for (int w = 0; w < kWaves; w++) {
+      before += w < (int)(tid / kWave) ? red[w] : 0u;
+      all += red[w];
+    }
+    __syncthreads();
+    if (i < L1) a.out_off[i] = min(base + before + x - cap, f.out_cap);
+    base += all;
+  }
+  if (tid == 0) a.out_off[L1] = min(base, f.out_cap);  // (the next workgroup writes the same value)
+  __threadfence_block();  // this range's parse and layout, for the decode's other waves
+  __syncthreads();
   StrFinish str;
   str.kind = a.sc_kind;
   str.start = a.sc_start;
@@ -2184,8 +2165,9 @@ __global__ __launch_bounds__(kT) void read_fallback_kernel(RsFallback f, const u
   str.hend = a.sc_hend;
   str.blk = a.blk;
   str.out_cap = f.out_cap;
-  str.finish_needed = f.finish_needed;
+  str.finish_needed = f.wg_fin + b;
   str.gen = a.gen;
+  str.local = true;
   decode_body<true>(sm, a.blk, a.sc_start, a.sc_hend, str, 0, n, a.out, a.out_off, 0, a.out_len, a.status, g_lut1,
                     g_lut2, g_len, per_block, tl0);
 }
@@ -2243,7 +2225,7 @@ hipError_t launch_read_fused(const DevTables &t, const uint8_t *blk, uint64_t bl
                              const uint64_t *limit, const uint8_t *prefix, uint64_t n, uint8_t *out,
                              uint64_t *out_off, uint32_t *out_len, uint8_t *status, uint64_t *next,
                              uint64_t *sc_start, uint32_t *sc_hend, uint8_t *sc_kind, uint64_t *fallback,
-                             uint64_t *bar, uint64_t gen, hipStream_t s) {
+                             uint64_t gen, hipStream_t s) {
   if (n == 0) return hipSuccess;
   const uint64_t cus = (uint64_t)dev::device_cus();
   const uint64_t slots = cus * kWaves;
@@ -2257,7 +2239,7 @@ hipError_t launch_read_fused(const DevTables &t, const uint8_t *blk, uint64_t bl
   const uint64_t per_block = (((n + cus - 1) / cus + tl - 1) / tl) * tl;
   const unsigned grid = (unsigned)((n + per_block - 1) / per_block);
   RsArgs a{blk, blk_len, pos, limit, prefix, n, out, out_off, next, out_len, status, sc_start, sc_hend, sc_kind,
-           fallback, gen, bar};
+           fallback, gen};
   read_fused_kernel<<<dim3(grid), dim3(kT), 0, s>>>(a, t.lut1, t.lut2, t.len, per_block, (uint32_t)tl);
   return hipGetLastError();
 }
@@ -2268,8 +2250,7 @@ hipError_t launch_read_fallback(const DevTables &t, const uint8_t *blk, uint64_t
                                 const uint64_t *limit, const uint8_t *prefix, uint64_t n, uint8_t *out,
                                 uint64_t out_cap, uint64_t *out_off, uint32_t *out_len, uint8_t *status,
                                 uint64_t *next, uint64_t *sc_start, uint32_t *sc_hend, uint8_t *sc_kind,
-                                uint64_t *fallback, uint64_t *order_bad, uint64_t *finish_needed, uint64_t *bar,
-                                uint64_t *wg_sums, uint64_t gen, hipStream_t s) {
+                                uint64_t *fallback, uint64_t *wg_agg, uint64_t *wg_fin, uint64_t gen, hipStream_t s) {
   if (n == 0) return hipSuccess;
   const uint64_t cus = (uint64_t)dev::device_cus();
   const uint64_t slots = cus * kWaves;
@@ -2279,8 +2260,8 @@ hipError_t launch_read_fallback(const DevTables &t, const uint8_t *blk, uint64_t
   const unsigned grid = (unsigned)((n + per_block - 1) / per_block);
   if (grid > kReadFallbackMaxWgs) return hipErrorInvalidConfiguration;
   RsFallback f{RsArgs{blk, blk_len, pos, limit, prefix, n, out, out_off, next, out_len, status, sc_start, sc_hend,
-                      sc_kind, fallback, gen, bar},
-               out_cap, order_bad, finish_needed, wg_sums};
+                      sc_kind, fallback, gen},
+               out_cap, wg_agg, wg_fin};
   read_fallback_kernel<<<dim3(grid), dim3(kT), 0, s>>>(f, t.lut1, t.lut2, t.len, per_block, (uint32_t)tl);
   return hipGetLastError();
 }

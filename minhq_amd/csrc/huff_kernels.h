@@ -54,6 +54,9 @@ struct StrFinish {
   uint64_t out_cap = 0;
   const uint64_t *finish_needed = nullptr;
   uint64_t gen = 0;
+  // the workgroup's own range sets the tile-length means and the cut test
+  // (the fused read's fallback: no other workgroup's data is read)
+  bool local = false;
 };
 hipError_t launch_decode(const DevTables &t, const uint8_t *in, const uint64_t *in_off,
                          uint64_t in_bias, uint64_t n, uint8_t *out, const uint64_t *out_off,
@@ -69,19 +72,18 @@ hipError_t launch_read_fused(const DevTables &t, const uint8_t *blk, uint64_t bl
                              const uint64_t *limit, const uint8_t *prefix, uint64_t n, uint8_t *out,
                              uint64_t *out_off, uint32_t *out_len, uint8_t *status, uint64_t *next,
                              uint64_t *sc_start, uint32_t *sc_hend, uint8_t *sc_kind, uint64_t *fallback,
-                             uint64_t *bar, uint64_t gen, hipStream_t s);
-// The fallback of launch_read_fused, one launch that returns at
-// once unless *fallback == gen: parse, the scan (strings out of order) and
-// the decode of the multi-pass pipeline as phases between grid barriers.
-// bar: one word, zeroed by launch_read_fused's kernel; wg_sums:
-// kReadFallbackMaxWgs words.
+                             uint64_t gen, hipStream_t s);
+// The fallback of launch_read_fused, one launch that returns at once unless
+// *fallback == gen (strings out of block order): parse, the regions back to
+// back (a decoupled look-back over per-workgroup capacity sums) and the
+// decode, per workgroup range.  wg_agg / wg_fin: kReadFallbackMaxWgs words
+// each (no reset needed: the sums carry gen's low bits).
 constexpr unsigned kReadFallbackMaxWgs = 1024;
 hipError_t launch_read_fallback(const DevTables &t, const uint8_t *blk, uint64_t blk_len, const uint64_t *pos,
                                 const uint64_t *limit, const uint8_t *prefix, uint64_t n, uint8_t *out,
                                 uint64_t out_cap, uint64_t *out_off, uint32_t *out_len, uint8_t *status,
                                 uint64_t *next, uint64_t *sc_start, uint32_t *sc_hend, uint8_t *sc_kind,
-                                uint64_t *fallback, uint64_t *order_bad, uint64_t *finish_needed, uint64_t *bar,
-                                uint64_t *wg_sums, uint64_t gen, hipStream_t s);
+                                uint64_t *fallback, uint64_t *wg_agg, uint64_t *wg_fin, uint64_t gen, hipStream_t s);
 // out_off[i] = base + sum_{j<i} enc_len[j]; cap_off[i] = base + sum_{j<i} floor(8*enc_len[j]/5)
 // (either output may be null).  Scratch: offsets_scratch_bytes(n) bytes, or
 // null for a hipMallocAsync on `s`.

@@ -439,7 +439,7 @@ struct ReadLayout {
     kind = take_(n);
     flags = take_(24);  // order_bad, finish_needed, fallback (the fused pass)
     sums = take_(offsets_sums_scratch_bytes(n));
-    coop = take_(8 * (1 + kReadFallbackMaxWgs));  // the fused read's fallback: barrier word, workgroup sums
+    coop = take_(8 * 2 * kReadFallbackMaxWgs);  // the fused read's fallback: workgroup sums, raw flags
     total = o;
   }
 };
@@ -489,10 +489,10 @@ hipError_t launch_read_strings(const DevTables &t, const uint8_t *blk, uint64_t 
   if (kFused) {
     uint64_t *coop = (uint64_t *)(base + L.coop);
     TRY(launch_read_fused(t, blk, blk_len, pos, limit, prefix, n, out, out_off, out_len, status, next, sc.start,
-                          sc.hend, sc.kind, fallback, coop, gen, s));
+                          sc.hend, sc.kind, fallback, gen, s));
 #ifndef MHQ_X_NOFB  // timing experiment only (no fallback: wrong for strings out of order)
     TRY(launch_read_fallback(t, blk, blk_len, pos, limit, prefix, n, out, out_cap, out_off, out_len, status, next,
-                             sc.start, sc.hend, sc.kind, fallback, order_bad, finish_needed, coop, coop + 1, gen, s));
+                             sc.start, sc.hend, sc.kind, fallback, coop, coop + kReadFallbackMaxWgs, gen, s));
 #endif
     goto done;
   }
