@@ -10,7 +10,7 @@ through the C ABI (include/mhq_huff.h), inputs resident in HBM.  Rotating
 copies of every buffer (>= 1 GiB in all) keep the 256 MB Infinity Cache from
 serving a step's inputs from the previous step.
 
-Consecutive batches alternate over 3 HIP streams (--streams; batches are
+Consecutive batches alternate over 4 HIP streams (--streams; batches are
 independent, a slot always runs on the same stream): one batch's first
 kernels fill the CUs that the previous batch's decode leaves idle at its tail.
 
@@ -676,7 +676,7 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-extras", action="store_true")
     ap.add_argument("--no-configs", action="store_true", help="skip the full-size configs 4 and 5")
-    ap.add_argument("--streams", type=int, default=3, help="streams the batches alternate over")
+    ap.add_argument("--streams", type=int, default=4, help="streams the batches alternate over (4: the hardware queues a process gets)")
     ap.add_argument("--traffic", default=os.path.join(REPO, "profiles", "pmc_traffic.json"))
     args = ap.parse_args()
 
