@@ -62,8 +62,8 @@
 #ifndef MHQ_DEC_LONG1  // 0: only the step before the end test resolves codes of 13+ bits
 #define MHQ_DEC_LONG1 0
 #endif
-#ifndef MHQ_DEC_STEPS  // masked steps per end test of the probe loop
-#define MHQ_DEC_STEPS 2
+#ifndef MHQ_DEC_STEPS  // masked steps per end test of the probe loop (3 since r04c: north star -2.7 %, config 4 -7 %, print +3 %)
+#define MHQ_DEC_STEPS 3
 #endif
 #ifndef MHQ_DEC_NTLEN  // out_len / status as streaming stores (config 2 37.1 -> 35.7 us, config 3 32.9 -> 31.8)
 #define MHQ_DEC_NTLEN 1
