@@ -62,8 +62,8 @@
 #ifndef MHQ_DEC_LONG1  // 0: only the step before the end test resolves codes of 13+ bits
 #define MHQ_DEC_LONG1 0
 #endif
-#ifndef MHQ_DEC_STEPS  // masked steps per end test of the probe loop (3 since r04c: north star -2.7 %, config 4 -7 %, print +3 %)
-#define MHQ_DEC_STEPS 3
+#ifndef MHQ_DEC_STEPS  // masked steps per end test of the probe loop
+#define MHQ_DEC_STEPS 2
 #endif
 #ifndef MHQ_DEC_NTLEN  // out_len / status as streaming stores (config 2 37.1 -> 35.7 us, config 3 32.9 -> 31.8)
 #define MHQ_DEC_NTLEN 1
@@ -1893,13 +1893,13 @@ __global__ __launch_bounds__(kT) void read_fused_kernel(RsArgs a, const uint32_t
   uint32_t pd_m = 0, pd_lo = 0, pd_hi = 0, kinds = 0;
   uint8_t *pd_o = nullptr;
   uint32_t tl_j = 0;
-  // the fallback flag's low word (the gen counter), loaded a tile ahead: a
-  // wave stops once some wave has sent the call to the fallback
-  const uint32_t *fb = (const uint32_t *)a.fallback, gen32 = (uint32_t)a.gen;
-  uint32_t fb_seen = 0;
+  // the fallback word, loaded a tile ahead: a wave stops once some wave has
+  // sent the call to the fallback (the whole word is compared: the scratch
+  // holds stale data, whose low word may well equal a small gen counter)
+  uint64_t fb_seen = 0;
 
   while (tile < ntiles) {
-    if (__builtin_amdgcn_readfirstlane(fb_seen) == gen32) break;
+    if (uniform64(fb_seen) == a.gen) break;
     const uint64_t s = L0 + (uint64_t)tile * tl;
     const uint32_t cnt = (uint32_t)min((uint64_t)tl, L1 - s);
     uint64_t ps, pe;
@@ -1978,7 +1978,7 @@ __global__ __launch_bounds__(kT) void read_fused_kernel(RsArgs a, const uint32_t
       span(rn, L0 + (uint64_t)tile2 * tl, ps2, pe2);
       load_in(tin, a.blk, 0, ps2, pe2, lane);
     }
-    fb_seen = __builtin_nontemporal_load(fb + vzero());  // (after the input loads: waited for with them)
+    fb_seen = __builtin_nontemporal_load(a.fallback + vzero());  // (after the input loads: waited for with them)
     rt = rn;
     rs_load(rn, a, L0 + (uint64_t)tile3 * tl, L1, tl, lane);
     if (skip) {
