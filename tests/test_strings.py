@@ -265,6 +265,38 @@ def test_read_full_tiles_long_and_raw(codec, oracle_mod):
     assert int((np.asarray(st) == EOF).sum()) == sum(1 for i in range(n) if blk[pos[i]] in (0x80,))
 
 
+@pytest.mark.parametrize("order", ["block", "shuffled", "overlap"])
+def test_read_random_bytes_as_frames(codec, oracle_mod, order):
+    """Random octets read as frames at increasing positions: each string's
+    limit at or before the next one's pos (block order: the one-pass read),
+    the same strings shuffled (the one-launch fallback, regions back to back),
+    or random limits past the next pos (overlapping payloads: the fallback,
+    and regions past the output buffer come back NOSPACE) -- every other
+    string against the oracle's ReadString over [pos, limit)."""
+    NOSPACE = 3
+    rng = random.Random({"block": 51, "shuffled": 52, "overlap": 53}[order])
+    n = 30000
+    blk = bytes(rng.randrange(256) for _ in range(n * 12))
+    pos = sorted(rng.randrange(len(blk)) for _ in range(n))
+    nxt_pos = pos[1:] + [len(blk)]
+    lim = [min(p + rng.randrange(1, 200), len(blk) if order == "overlap" else q) for p, q in zip(pos, nxt_pos)]
+    pf = [rng.choice([7, 7, 5, 3, 1]) for _ in range(n)]
+    idx = list(range(n))
+    if order == "shuffled":
+        rng.shuffle(idx)
+    P, L, F = [pos[i] for i in idx], [lim[i] for i in idx], [pf[i] for i in idx]
+    vals, st, nxt = codec.read_strings(blk, P, F, L)
+    checked = 0
+    for k in range(n):
+        ref, rc, used = oracle_mod.read_string(blk[P[k]:L[k]], prefix=F[k], skip_bits=7 - F[k])
+        assert int(nxt[k]) == P[k] + used, (order, k)
+        if order == "overlap" and int(st[k]) == NOSPACE:
+            continue
+        assert (vals[k], int(st[k])) == (ref, _oracle_status(rc)), (order, k)
+        checked += 1
+    assert checked == n or (order == "overlap" and checked > 1000)
+
+
 def test_read_wild_pos_and_reverse_order_at_buffer_end(codec, oracle_mod):
     """strings read in reverse block order and header-error
     strings whose pos lies far past the block, with the block ending exactly
