@@ -62,8 +62,11 @@
 #ifndef MHQ_DEC_LONG1  // 0: only the step before the end test resolves codes of 13+ bits
 #define MHQ_DEC_LONG1 0
 #endif
-#ifndef MHQ_DEC_STEPS  // masked steps per end test of the probe loop
-#define MHQ_DEC_STEPS 2
+#ifndef MHQ_DEC_STEPS  // masked steps per end test of the probe loop (the plain decode)
+#define MHQ_DEC_STEPS 3
+#endif
+#ifndef MHQ_DEC_STEPS_GAPS  // the same for the in_end decode of framed strings (read_strings)
+#define MHQ_DEC_STEPS_GAPS 2
 #endif
 #ifndef MHQ_DEC_NTLEN  // out_len / status as streaming stores (config 2 37.1 -> 35.7 us, config 3 32.9 -> 31.8)
 #define MHQ_DEC_NTLEN 1
@@ -851,6 +854,10 @@ __device__ __forceinline__ void flush_lens(const WaveSmem &ws, uint64_t s, uint3
 template <bool kGaps>
 __device__ __forceinline__ void decode_piece(const Smem &sm, WaveSmem &ws, uint32_t m, uint32_t out_bytes,
                                              uint32_t lane, [[maybe_unused]] int tls = -1, uint32_t prio = 0) {
+  // masked steps per end test: 3 for the plain decode (north star -2.7 %,
+  // config 4 -7 %, print +3 %: profiles/r04c_decode_steps_ab.txt); the read
+  // path keeps 2 (one unexplained fault of a read test with 3)
+  constexpr int kSteps = kGaps ? MHQ_DEC_STEPS_GAPS : MHQ_DEC_STEPS;
   for (uint32_t c = lane; c < (out_bytes + 15u) >> 4; c += kWave) *(u32x4 *)(ws.out_w + 4u * c) = u32x4{0u, 0u, 0u, 0u};
 #ifdef MHQ_X_DBLZERO  // timing experiment: the zeroing twice
   wave_sync();
@@ -948,7 +955,7 @@ __device__ __forceinline__ void decode_piece(const Smem &sm, WaveSmem &ws, uint3
     while (__ballot(active)) {
       bool stop;
 #pragma unroll
-      for (int k = 1; k < MHQ_DEC_STEPS; k++) masked_step_lean<MHQ_DEC_LONG1 != 0>(sm, in, out, pend, stop);
+      for (int k = 1; k < kSteps; k++) masked_step_lean<MHQ_DEC_LONG1 != 0>(sm, in, out, pend, stop);
       const bool fin = masked_step_lean(sm, in, out, pend, stop);
       // stop: the EOS prefix (INVALID when a 31st bit of the literal follows);
       // left < 0: a code crossed the end (the piece is redone, below)
@@ -987,7 +994,7 @@ __device__ __forceinline__ void decode_piece(const Smem &sm, WaveSmem &ws, uint3
     while (active) {
       bool stop;
 #pragma unroll
-      for (int k = 1; k < MHQ_DEC_STEPS; k++) MHQ_WSTEP(MHQ_DEC_LONG1 != 0);
+      for (int k = 1; k < kSteps; k++) MHQ_WSTEP(MHQ_DEC_LONG1 != 0);
       if (MHQ_WSTEP(true)) {
         const uint32_t r = in.left < 0 ? kRedo : (out.optr(ws.out_w) - ost) | ((uint32_t)(in.left > kEosOnes) << 31);
         rA = onB ? rA : r;
@@ -1015,7 +1022,7 @@ __device__ __forceinline__ void decode_piece(const Smem &sm, WaveSmem &ws, uint3
     while (active) {
       bool stop;
 #pragma unroll
-      for (int k = 1; k < MHQ_DEC_STEPS; k++) masked_step_lean<MHQ_DEC_LONG1 != 0>(sm, in, out, pend, stop);
+      for (int k = 1; k < kSteps; k++) masked_step_lean<MHQ_DEC_LONG1 != 0>(sm, in, out, pend, stop);
       if (masked_step_lean(sm, in, out, pend, stop)) {
         // stop: the EOS prefix (INVALID when a 31st bit of the literal follows);
         // left < 0: a code crossed the end (the piece is redone, below)
@@ -1061,7 +1068,7 @@ __device__ __forceinline__ void decode_piece(const Smem &sm, WaveSmem &ws, uint3
       // consumed at the EOS prefix; `left` stays negative, the word held
       // back), so the last step's result covers them all
 #pragma unroll
-      for (int k = 1; k < MHQ_DEC_STEPS; k++) masked_step<MHQ_DEC_LONG1 != 0>(sm, ws.out_w, in, out, pend, stop);
+      for (int k = 1; k < kSteps; k++) masked_step<MHQ_DEC_LONG1 != 0>(sm, ws.out_w, in, out, pend, stop);
       if (masked_step(sm, ws.out_w, in, out, pend, stop)) {
         // stop: the EOS prefix at p (INVALID when a 31st bit of the literal follows)
         const uint32_t r = in.left < 0 ? kRedo : (out.optr() - ost) | ((uint32_t)(in.left > kEosOnes) << 31);
