@@ -41,8 +41,8 @@
 #ifndef MHQ_ENC_OUTCAP  // output staging slice (bytes, encode only)
 #define MHQ_ENC_OUTCAP 20480
 #endif
-#ifndef MHQ_ENC_BRANCHY  // 1: the bit writer ORs a word out under a per-code branch (0: branch free, config 4 -7 %, config 2 +10 %)
-#define MHQ_ENC_BRANCHY 1
+#ifndef MHQ_ENC_BRANCHY  // 1: the bit writer ORs a word out under a per-code branch (0, branch free: since r04e, config 2 -1 %, north star -0.7 to -1.3 %)
+#define MHQ_ENC_BRANCHY 0
 #endif
 #ifndef MHQ_ENC_NTST  // encode_len's lengths and the cooperative encode's whole chunks as streaming stores (config 5 encode 162.8 -> 154.9 us)
 #define MHQ_ENC_NTST 1
