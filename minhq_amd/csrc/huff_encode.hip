@@ -472,7 +472,10 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu((kT / 64 * M
 // literal of < 2^32 bits).  Every lane does the same work whatever the
 // length mix, and long literals are spread over the wave.
 constexpr int kLenT = kLenSumBlock;  // 4 waves of 64 literals
-constexpr int kLenRB = 4;            // rounds whose loads are issued together
+#ifndef MHQ_LEN_RB  // encode_len: rounds whose loads are issued together
+#define MHQ_LEN_RB 4
+#endif
+constexpr int kLenRB = MHQ_LEN_RB;
 constexpr uint32_t kRound = kWave * 16;  // bytes per round
 
 // Slot of P(x) in a wave's row: lane l's 16 values (4 chunks of 4) go to
