@@ -5,10 +5,12 @@ Run with the process's queues limited to a few CUs (HSA_CU_MASK), so that
 the fallback kernel's grid (one workgroup per CU of the device) cannot be
 resident at once: its workgroups wait only for lower-numbered ones (the
 decoupled look-back), so the call completes with the same results as without
-the mask.  Prints one JSON line (status counts and a checksum of the output).
+the mask.  Prints one JSON line (status counts and checksums of the strings
+and next positions, to compare between a masked and an unmasked run).
 
     HSA_CU_MASK=0:0-31 python3 tools/fallback_masked.py
 """
+import hashlib
 import json
 import os
 import random
@@ -21,21 +23,20 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 from minhq_amd import _lib, hc  # noqa: E402
-from oracle import oracle  # noqa: E402
 
 
 def main():
     rng = random.Random(5)
     alpha = b"abcdefghijklmnopqrstuvwxyz0123456789-_./:;=, "
     n = 1 << 16
-    frames = [oracle.write_string(bytes(rng.choice(alpha) for _ in range(rng.randint(1, 40))), prefix=7, choice=1)
-              for _ in range(n)]
+    codec = hc.Codec(devices=[0])
+    lits = [bytes(rng.choice(alpha) for _ in range(rng.randint(1, 40))) for _ in range(n)]
+    frames = codec.write_strings(lits, [7] * n, None, hc.HuffmanCodingAlways)
     pos = np.zeros(n, dtype=np.uint64)
     pos[1:] = np.cumsum([len(f) for f in frames])[:-1]
     blk = b"".join(frames)
     P = pos[::-1].copy()  # reverse block order: the fused pass sends the call to the fallback
     dev = torch.device("cuda:0")
-    codec = hc.Codec(devices=[0])
     t_blk = torch.frombuffer(bytearray(blk), dtype=torch.uint8).to(dev)
     t_pos = torch.from_numpy(P.view(np.int64)).to(dev)
     t_lim = torch.full((n,), len(blk), dtype=torch.int64, device=dev)
@@ -53,10 +54,11 @@ def main():
     counts = {int(k): int(v) for k, v in zip(*np.unique(s, return_counts=True))}
     oo, ol, o = out_off.cpu().numpy(), out_len.cpu().numpy(), out.cpu().numpy()
     got = [o[oo[k]:oo[k] + ol[k]].tobytes() for k in range(n)]
-    want = [oracle.read_string(blk[int(q):int(q) + 100], prefix=7)[0] for q in P]
+    order = {int(q): i for i, q in enumerate(pos)}
     print(json.dumps({"cu_mask": os.environ.get("HSA_CU_MASK", ""), "strings": n, "seconds": round(dt, 3),
                       "status_counts": counts, "ok": int(counts.get(_lib.MHQ_STR_OK, 0)),
-                      "values_equal_oracle": got == want,
+                      "values_equal_written": got == [lits[order[int(q)]] for q in P],
+                      "strings_sha": hashlib.sha256(b"\0".join(got)).hexdigest()[:16],
                       "next_sum": int(nxt.cpu().numpy().sum())}), flush=True)
     codec.close()
 
