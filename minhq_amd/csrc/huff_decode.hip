@@ -65,6 +65,9 @@
 #ifndef MHQ_DEC_STEPS  // masked steps per end test of the probe loop (the plain decode)
 #define MHQ_DEC_STEPS 3
 #endif
+#ifndef MHQ_DEC_LONGMID
+#define MHQ_DEC_LONGMID 0
+#endif
 #ifndef MHQ_DEC_STEPS_GAPS  // the same for the in_end decode of framed strings (read_strings)
 #define MHQ_DEC_STEPS_GAPS 2
 #endif
@@ -993,8 +996,14 @@ __device__ __forceinline__ void decode_piece(const Smem &sm, WaveSmem &ws, uint3
     bool onB = !roomA, active = roomA || roomB;
     while (active) {
       bool stop;
+#if MHQ_DEC_LONGMID  // experiment: the steps after the first resolve long codes too
+      MHQ_WSTEP(MHQ_DEC_LONG1 != 0);
+#pragma unroll
+      for (int k = 2; k < kSteps; k++) MHQ_WSTEP(true);
+#else
 #pragma unroll
       for (int k = 1; k < kSteps; k++) MHQ_WSTEP(MHQ_DEC_LONG1 != 0);
+#endif
       if (MHQ_WSTEP(true)) {
         const uint32_t r = in.left < 0 ? kRedo : (out.optr(ws.out_w) - ost) | ((uint32_t)(in.left > kEosOnes) << 31);
         rA = onB ? rA : r;
