@@ -97,4 +97,8 @@ hipError_t launch_decode(const DevTables &t, const uint8_t *in, const uint64_t *
   return hipGetLastError();
 }
 
+#ifdef MHQ_DBG_BOUNDS
+MHQ_DBG_READER(mhq_dbg_bounds_decode)
+#endif
+
 }  // namespace mhq

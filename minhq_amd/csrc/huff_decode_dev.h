@@ -65,6 +65,39 @@ struct Smem {
   WaveSmem w[kWaves];
 };
 
+#ifdef MHQ_DBG_BOUNDS
+// Diagnostic build (-DMHQ_DBG_BOUNDS): the bounds of the LDS records, the
+// fast loop's output word and the global stores of the decode and read path
+// are checked where they are formed; a violation is recorded -- a code and two
+// values, the first 16 -- never faulted on.  mhq_dbg_bounds_decode /
+// mhq_dbg_bounds_read (one per translation unit) read and clear the records.
+__device__ unsigned long long g_dbg[1 + 3 * 16];
+__device__ __noinline__ void dbg_fail(uint32_t code, uint64_t a, uint64_t b) {
+  const unsigned long long k = atomicAdd(&g_dbg[0], 1ull);
+  if (k < 16) {
+    g_dbg[1 + 3 * k] = code;
+    g_dbg[2 + 3 * k] = a;
+    g_dbg[3 + 3 * k] = b;
+  }
+}
+#define DBG_CHECK(c, code, a, b)                                         \
+  do {                                                                   \
+    if (!(c)) dbg_fail((code), (uint64_t)(a), (uint64_t)(b));            \
+  } while (0)
+#define MHQ_DBG_READER(name)                                                                  \
+  extern "C" int name(unsigned long long *out, int n) {                                       \
+    unsigned long long h[1 + 3 * 16];                                                         \
+    if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_dbg), sizeof(h)) != hipSuccess) return -1;        \
+    for (int i = 0; i < n && i < 1 + 3 * 16; i++) out[i] = h[i];                              \
+    unsigned long long z[1 + 3 * 16] = {0};                                                   \
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_dbg), z, sizeof(z)) == hipSuccess ? 0 : -1;         \
+  }
+#else
+#define DBG_CHECK(c, code, a, b) \
+  do {                           \
+  } while (0)
+#endif
+
 // A code of 13..30 bits, or the all-ones EOS prefix (c >= 30), at the top of
 // the 32 stream bits `win`: its symbol and length, length 0 for the EOS prefix.
 __device__ __forceinline__ uint32_t long_code(const uint16_t *lut2, uint32_t win, uint32_t &sym) {
@@ -335,6 +368,7 @@ __device__ __noinline__ uint32_t decode_checked(const Smem &sm, WaveSmem &ws, ui
     in.bb <<= cons & 63u;
     in.p += cons;
     fin = c8 == 0;
+    DBG_CHECK(out.ow < (uint32_t)kWOut / 4u + 4u, 5, out.ow, oend);
     out.flush(ws.out_w);
   }
   const uint32_t oend_got = out.optr();
@@ -600,6 +634,20 @@ __device__ __forceinline__ void decode_piece(const Smem &sm, WaveSmem &ws, uint3
   A.load(ws, hasA ? ws.order[lane] : 0u);
   B.load(ws, hasB ? ws.order[2u * kWave - 1u - lane] : 0u);
   const uint32_t ostartA = A.optr, ostartB = B.optr;
+#ifdef MHQ_DBG_BOUNDS
+  {
+    const uint32_t span = (ws.rec[m] & 0xffffu) * 8u;  // the staged input's end (bits)
+    if (hasA) {
+      DBG_CHECK(A.p <= A.endbit && A.endbit <= span, 2, A.p | (uint64_t)A.endbit << 32, span);
+      DBG_CHECK(A.optr <= A.oend && A.oend <= out_bytes, 3, A.optr | (uint64_t)A.oend << 32, out_bytes);
+    }
+    if (hasB) {
+      DBG_CHECK(B.p <= B.endbit && B.endbit <= span, 2, B.p | (uint64_t)B.endbit << 32, span);
+      DBG_CHECK(B.optr <= B.oend && B.oend <= out_bytes, 3, B.optr | (uint64_t)B.oend << 32, out_bytes);
+    }
+    DBG_CHECK(out_bytes <= (uint32_t)kWOut, 4, out_bytes, m);
+  }
+#endif
   TL(tls);
   set_loop_prio(prio);
   // Every literal runs the masked loop to its end (ones past the end: no end
@@ -642,6 +690,7 @@ __device__ __forceinline__ void decode_piece(const Smem &sm, WaveSmem &ws, uint3
         ost = ostartB;
         onB = true;
       }
+      DBG_CHECK((uint32_t)(pend.p - ws.out_w) < (uint32_t)kWOut / 4u + 4u, 1, pend.p - ws.out_w, kSteps);
     }
     atomicOr(pend.p, pend.v);
   }
@@ -850,6 +899,7 @@ __device__ void decode_tile_long(const Smem &sm, WaveSmem &ws, const uint8_t *__
   OutAccG acc;
   acc.init(0);
   uint32_t ostart = 0;
+  [[maybe_unused]] uint64_t oreg = 0;  // the literal's region (bytes; MHQ_DBG_BOUNDS)
   // next literal of this lane (roomy ones stay; the rest are done at once from global memory)
   auto next_lit = [&]() {
     have = false;
@@ -876,6 +926,7 @@ __device__ void decode_tile_long(const Smem &sm, WaveSmem &ws, const uint8_t *__
         gout = (uint32_t *)(o - ((uintptr_t)o & 3u));  // pointer arithmetic keeps it global: no flat stores
         ostart = (uint32_t)((uintptr_t)o & 3u);
         acc.init(ostart, (uint32_t)((uintptr_t)gout >> 2) & 3u);
+        oreg = oe - ob;
         rel = 0;
         have = true;
         return;
@@ -898,6 +949,7 @@ __device__ void decode_tile_long(const Smem &sm, WaveSmem &ws, const uint8_t *__
       const uint8_t *a16 = a - delta;
       src = (uint64_t)(uintptr_t)a16;
       const uint8_t *last = in + (ie - in_bias) - 1;  // the literal's last byte
+      DBG_CHECK(a <= last, 8, rel, ie - ib);
       nck = min((uint32_t)(((uintptr_t)last - (uintptr_t)a16) >> 4) + 1u, kLongWords / 4u);
       p = delta * 8u + (uint32_t)(rel & 7u);
       endw = p + (uint32_t)((ie - ib) * 8u - rel);  // the literal's end in window bits (may lie beyond)
@@ -934,6 +986,7 @@ __device__ void decode_tile_long(const Smem &sm, WaveSmem &ws, const uint8_t *__
       if (stopped || ends_here) {
         const uint32_t st = stopped ? bad : end_checked_g<BitBufS>(sm, win, bin.p, endw, acc, gout, swz);
         uint32_t got = acc.optr() - ostart, st2 = st;
+        DBG_CHECK(got <= oreg, 6, got, oreg);
         acc.finish(gout);
         if (kGaps && str_kind) str_outcome(str_kind, s + j, got, st2);
         out_len[s + j] = got;
@@ -1203,6 +1256,7 @@ __device__ __forceinline__ void decode_body(Smem &sm, const uint8_t *__restrict_
           if (take == 0 && (kd & kDeclared)) {
             status[i] = (uint8_t)kStrEof;  // the block ended before the payload: io.EOF
           } else if (take) {
+            DBG_CHECK(o0 + take <= out_off[i + 1], 13, o0, take);
             copy_bytes(out + (o0 - out_bias), str.blk + st0, take);
             out_len[i] = (uint32_t)take;
           }

@@ -72,12 +72,13 @@ hipError_t launch_read_fused(const DevTables &t, const uint8_t *blk, uint64_t bl
                              const uint64_t *limit, const uint8_t *prefix, uint64_t n, uint8_t *out,
                              uint64_t *out_off, uint32_t *out_len, uint8_t *status, uint64_t *next,
                              uint64_t *sc_start, uint32_t *sc_hend, uint8_t *sc_kind, uint64_t *fallback,
-                             uint64_t gen, hipStream_t s);
+                             uint64_t *wg_agg, uint64_t gen, hipStream_t s);
 // The fallback of launch_read_fused, one launch that returns at once unless
 // *fallback == gen (strings out of block order): parse, the regions back to
 // back (a decoupled look-back over per-workgroup capacity sums) and the
 // decode, per workgroup range.  wg_agg / wg_fin: kReadFallbackMaxWgs words
-// each (no reset needed: the sums carry gen's low bits).
+// each; launch_read_fused clears wg_agg (the look-back slots) for it, and the
+// published sums carry a never-zero tag of gen.
 constexpr unsigned kReadFallbackMaxWgs = 1024;
 hipError_t launch_read_fallback(const DevTables &t, const uint8_t *blk, uint64_t blk_len, const uint64_t *pos,
                                 const uint64_t *limit, const uint8_t *prefix, uint64_t n, uint8_t *out,

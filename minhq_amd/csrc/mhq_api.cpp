@@ -795,8 +795,14 @@ int mhq_read_strings(mhq_ctx *ctx, const uint8_t *blk, uint64_t blk_len, const u
   MHQ_TRY(dlen.alloc(n));
   MHQ_TRY(dst.alloc(n));
   MHQ_TRY(dnext.alloc(n));
-  MHQ_TRY(mhq::launch_read_strings(d->tables, dblk.p, blk_len, dpos.p, dlim.p, dprefix.p, n, dout.p, out_cap,
-                                   doff.p, dlen.p, dst.p, dnext.p, s));
+  {
+    // the per-stream scratch, as the device form takes it (no stream-ordered
+    // allocation and free per call; without a cached buffer the launcher
+    // allocates in stream order)
+    ScratchLease lease(d, s, n ? mhq::read_strings_scratch_bytes(n, blk_len) : 0);
+    MHQ_TRY(mhq::launch_read_strings(d->tables, dblk.p, blk_len, dpos.p, dlim.p, dprefix.p, n, dout.p, out_cap,
+                                     doff.p, dlen.p, dst.p, dnext.p, s, lease.p));
+  }
   MHQ_TRY(doff.get(out_off, n + 1, s));
   MHQ_TRY(hipStreamSynchronize(s));
   MHQ_TRY(dout.get(out, std::min<uint64_t>(out_off[n], out_cap), s));

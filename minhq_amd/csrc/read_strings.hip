@@ -39,6 +39,7 @@ struct RsArgs {
   uint8_t *sc_kind;
   uint64_t *fallback;
   uint64_t gen;
+  uint64_t *wg_agg;  // the fallback's look-back slots: cleared here (workgroup 0), kReadFallbackMaxWgs words
 };
 
 struct RsTile {  // pos / limit / prefix of strings s + 2 lane + {0, 1}; pos of string s + tile
@@ -142,6 +143,12 @@ __global__ __launch_bounds__(kT) void read_fused_kernel(RsArgs a, const uint32_t
   const uint64_t L1 = min(L0 + per_block, a.n);
   WaveSmem &ws = sm.w[wave];
   const uint64_t blk_len = a.blk_len;
+  // the fallback's look-back slots start every call cleared (stream order
+  // puts this before the fallback launch): a slot then holds this call's tag
+  // or 0, never stale data -- the per-stream scratch is shared with other
+  // calls and entry points, whose words could otherwise carry a matching tag
+  if (blockIdx.x == 0)
+    for (uint32_t g = tid; g < kReadFallbackMaxWgs; g += kT) a.wg_agg[g] = 0;
   // a tile's byte span, clamped to the block (empty past the range)
   auto span = [&](const RsTile &t, uint64_t s, uint64_t &ps, uint64_t &pe) {
     ps = pe = 0;
@@ -197,6 +204,7 @@ __global__ __launch_bounds__(kT) void read_fused_kernel(RsArgs a, const uint32_t
     uint8_t *oa = a.out + rs0;
     const uint32_t idelta = (uint32_t)((uintptr_t)ia & 15u), odelta = (uint32_t)((uintptr_t)oa & 15u);
     bool fits = pe >= ps && (pe - ps) + idelta <= (uint64_t)kWIn && (rs1 - rs0) + odelta <= (uint64_t)kWOut;
+    DBG_CHECK(!fits || rs1 <= region_at(blk_len), 10, rs1, blk_len);
     __builtin_amdgcn_s_setprio(kPhasePrio);
     uint32_t tile4 = 0;
     if (lane == 0) tile4 = atomicAdd(&sm.next_tile, 1u);
@@ -270,6 +278,12 @@ __global__ __launch_bounds__(kT) void read_fused_kernel(RsArgs a, const uint32_t
     if (skip) {
     } else if (fits) {
       const uint32_t out_bytes = (uint32_t)(rs1 - rs0) + odelta;
+#ifdef MHQ_DBG_BOUNDS
+      for (uint32_t j = lane; j < cnt; j += kWave)
+        DBG_CHECK((ws.rec[j] & 0xffffu) <= ws.len[j] && ws.len[j] <= (uint32_t)(pe - ps) + idelta &&
+                      (ws.rec[j] >> 16) <= (ws.rec[j + 1] >> 16),
+                  11, ws.rec[j] | (uint64_t)ws.rec[j + 1] << 32, ws.len[j] | (uint64_t)(pe - ps + idelta) << 32);
+#endif
       decode_piece<true>(sm, ws, cnt, out_bytes, lane, -1, tl_j < 2u ? 1u : 0u);
       // raw payloads into their regions
 #pragma unroll
@@ -277,6 +291,7 @@ __global__ __launch_bounds__(kT) void read_fused_kernel(RsArgs a, const uint32_t
         const uint32_t j = 2u * lane + (uint32_t)h, take = h ? raw1 : raw0;
         if (j < cnt && ((kinds >> (4 * h)) & 3u) == 0u) {
           const uint32_t r = ws.rec[j], x = r & 0xffffu, y = r >> 16;
+          DBG_CHECK(y + take <= out_bytes && x + take <= (uint32_t)(pe - ps) + idelta, 14, y + take, x + take);
           uint8_t *o = (uint8_t *)ws.out_w;
           for (uint32_t k = 0; k < take; k++) o[y + k] = (uint8_t)slice_byte(ws, x + k);
           ws.len[j] = take;
@@ -308,6 +323,7 @@ __global__ __launch_bounds__(kT) void read_fused_kernel(RsArgs a, const uint32_t
         if ((kd & 3u) != 0u) continue;
         const uint64_t st0 = a.sc_start[i], take = a.next[i] - st0;
         if (take) {
+          DBG_CHECK(a.out_off[i] + take <= region_at(blk_len) && st0 + take <= blk_len, 12, a.out_off[i], take);
           copy_bytes(a.out + a.out_off[i], a.blk + st0, take);
           a.out_len[i] = (uint32_t)take;
         } else if (kd & kDeclared) {
@@ -347,10 +363,14 @@ __global__ __launch_bounds__(kT) void read_fused_kernel(RsArgs a, const uint32_t
 struct RsFallback {
   RsArgs a;
   uint64_t out_cap;
-  uint64_t *wg_agg;  // per workgroup: gen's low 24 bits << 40 | capacity sum
+  uint64_t *wg_agg;  // per workgroup: agg_tag(gen) | capacity sum (0 until published; cleared by the fused pass)
   uint64_t *wg_fin;  // per workgroup: gen when its range holds a raw string
 };
 constexpr uint64_t kAggBits = 40;  // a workgroup's capacity sum < 2^40
+// A published sum's tag: 23 bits of the call's generation number and a set
+// bit, never 0, so a cleared slot never matches (and the read_fused_kernel
+// clears every slot before this launch).
+__device__ __forceinline__ uint64_t agg_tag(uint64_t gen) { return ((gen & 0x7fffffull) | 0x800000ull) << kAggBits; }
 
 // Sum of v over the workgroup (every thread gets it); red: kWaves words.
 __device__ __forceinline__ uint64_t wg_sum(uint64_t v, uint64_t *red) {
@@ -376,7 +396,7 @@ __global__ __launch_bounds__(kT) void read_fallback_kernel(RsFallback f, const u
   const uint32_t tid = threadIdx.x, b = blockIdx.x;
   const uint64_t n = a.n, blk_len = a.blk_len;
   const uint64_t L0 = (uint64_t)b * per_block, L1 = min(L0 + per_block, n);
-  const uint64_t tag = (a.gen & 0xffffffull) << kAggBits;
+  const uint64_t tag = agg_tag(a.gen);
   // parse (read_parse_kernel's rules, str_frame.hip) of [L0, L1] -- string L1
   // too (its payload start is in_off[L1], read by this range's last tile; its
   // own workgroup writes the same value)
@@ -466,7 +486,7 @@ hipError_t launch_read_fused(const DevTables &t, const uint8_t *blk, uint64_t bl
                              const uint64_t *limit, const uint8_t *prefix, uint64_t n, uint8_t *out,
                              uint64_t *out_off, uint32_t *out_len, uint8_t *status, uint64_t *next,
                              uint64_t *sc_start, uint32_t *sc_hend, uint8_t *sc_kind, uint64_t *fallback,
-                             uint64_t gen, hipStream_t s) {
+                             uint64_t *wg_agg, uint64_t gen, hipStream_t s) {
   if (n == 0) return hipSuccess;
   const uint64_t cus = (uint64_t)dev::device_cus();
   const uint64_t slots = cus * kWaves;
@@ -480,7 +500,7 @@ hipError_t launch_read_fused(const DevTables &t, const uint8_t *blk, uint64_t bl
   const uint64_t per_block = (((n + cus - 1) / cus + tl - 1) / tl) * tl;
   const unsigned grid = (unsigned)((n + per_block - 1) / per_block);
   RsArgs a{blk, blk_len, pos, limit, prefix, n, out, out_off, next, out_len, status, sc_start, sc_hend, sc_kind,
-           fallback, gen};
+           fallback, gen, wg_agg};
   read_fused_kernel<<<dim3(grid), dim3(kT), 0, s>>>(a, t.lut1, t.lut2, t.len, per_block, (uint32_t)tl);
   return hipGetLastError();
 }
@@ -501,10 +521,14 @@ hipError_t launch_read_fallback(const DevTables &t, const uint8_t *blk, uint64_t
   const unsigned grid = (unsigned)((n + per_block - 1) / per_block);
   if (grid > kReadFallbackMaxWgs) return hipErrorInvalidConfiguration;
   RsFallback f{RsArgs{blk, blk_len, pos, limit, prefix, n, out, out_off, next, out_len, status, sc_start, sc_hend,
-                      sc_kind, fallback, gen},
+                      sc_kind, fallback, gen, wg_agg},
                out_cap, wg_agg, wg_fin};
   read_fallback_kernel<<<dim3(grid), dim3(kT), 0, s>>>(f, t.lut1, t.lut2, t.len, per_block, (uint32_t)tl);
   return hipGetLastError();
 }
+
+#ifdef MHQ_DBG_BOUNDS
+MHQ_DBG_READER(mhq_dbg_bounds_read)
+#endif
 
 }  // namespace mhq

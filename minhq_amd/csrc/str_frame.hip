@@ -13,6 +13,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <cstdlib>
 
 #include "huff_common.h"
 #include "huff_kernels.h"
@@ -446,6 +447,19 @@ struct ReadLayout {
 
 }  // namespace
 
+// Test hook (MHQ_DEBUG_POISON_SCRATCH set in the environment): stale scratch
+// contents that could once be mistaken for this call's flags.  The fallback
+// word gets gen with its high half inverted (its low word equals gen's low
+// word: the round-4 fused pass compared only that), and every look-back slot
+// a capacity sum under the round-4 tag of gen (gen's low 24 bits).  The
+// whole-word compare and the cleared, never-zero tags make both harmless
+// (tests/test_strings.py::test_read_poisoned_scratch).
+__global__ void read_poison_kernel(uint64_t *fallback, uint64_t *wg_agg, uint64_t gen) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i == 0) *fallback = gen ^ 0xffffffff00000000ull;
+  if (i < kReadFallbackMaxWgs) wg_agg[i] = ((gen & 0xffffffull) << 40) | (12345u + 7u * i);
+}
+
 #ifndef MHQ_RS_FUSED  // read_strings: 1 the one-pass kernel, the multi-pass pipeline as its fallback
 #define MHQ_RS_FUSED 1
 #endif
@@ -488,8 +502,12 @@ hipError_t launch_read_strings(const DevTables &t, const uint8_t *blk, uint64_t 
   // launch that returns at once unless the pass stored gen to *fallback
   if (kFused) {
     uint64_t *coop = (uint64_t *)(base + L.coop);
+    if (getenv("MHQ_DEBUG_POISON_SCRATCH")) {
+      read_poison_kernel<<<(kReadFallbackMaxWgs + 255) / 256, 256, 0, s>>>(fallback, coop, gen);
+      TRY(hipGetLastError());
+    }
     TRY(launch_read_fused(t, blk, blk_len, pos, limit, prefix, n, out, out_off, out_len, status, next, sc.start,
-                          sc.hend, sc.kind, fallback, gen, s));
+                          sc.hend, sc.kind, fallback, coop, gen, s));
 #ifndef MHQ_X_NOFB  // timing experiment only (no fallback: wrong for strings out of order)
     TRY(launch_read_fallback(t, blk, blk_len, pos, limit, prefix, n, out, out_cap, out_off, out_len, status, next,
                              sc.start, sc.hend, sc.kind, fallback, coop, coop + kReadFallbackMaxWgs, gen, s));

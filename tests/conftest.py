@@ -31,3 +31,25 @@ def oracle_mod():
 
     oracle.build()
     return oracle
+
+
+@pytest.fixture(autouse=True)
+def _dbg_bounds_records():
+    """With MHQ_DBG_BOUNDS_CHECK=1 and a -DMHQ_DBG_BOUNDS build of the library
+    (MHQ_LIB_PATH), every test ends by reading the kernels' bounds records
+    (huff_decode_dev.h: LDS records, the fast loop's output word, the decode
+    and read path's global stores): none may have been recorded."""
+    yield
+    if os.environ.get("MHQ_DBG_BOUNDS_CHECK") != "1":
+        return
+    import ctypes
+
+    from minhq_amd import _lib
+
+    L = _lib.load()
+    for name in ("mhq_dbg_bounds_decode", "mhq_dbg_bounds_read"):
+        fn = getattr(L, name)
+        buf = (ctypes.c_ulonglong * 49)()
+        assert fn(buf, 49) == 0, name
+        recs = [(int(buf[1 + 3 * k]), hex(buf[2 + 3 * k]), hex(buf[3 + 3 * k])) for k in range(min(16, int(buf[0])))]
+        assert int(buf[0]) == 0, f"{name}: {int(buf[0])} bounds violations, first {recs}"

@@ -396,3 +396,63 @@ def test_read_regions_layout(codec, oracle_mod, order):
             assert oo[k + 1] - oo[k] == cap, k
     if order == "block":
         assert oo[n] == L * 8 // 5
+
+
+@pytest.mark.parametrize("order", ["in_order", "runs"])
+def test_read_poisoned_scratch(codec, oracle_mod, monkeypatch, order):
+    """Stale scratch that matches the call's flags in their round-4 form
+    (MHQ_DEBUG_POISON_SCRATCH, str_frame.hip): a fallback word whose LOW word
+    equals the call's generation number -- round 4's fused pass compared only
+    that and stopped its waves, while the fallback, comparing all 64 bits, did
+    nothing: strings left unwritten -- and look-back slots carrying round 4's
+    tag of the call with garbage sums -- its fallback added those up: regions
+    laid out wrong.  2^19 strings, so every wave of the fused pass has two
+    tiles; in block order (the fused pass alone) and in shuffled runs of 300
+    (the fallback, 255 workgroups looking back).  The device outputs start as
+    sentinels; every string equals the host call's result (unpoisoned), and a
+    sample the oracle's."""
+    import numpy as np
+    import torch
+
+    rng = random.Random(36 if order == "in_order" else 37)
+    alpha = b"abcdefghijklmnopqrstuvwxyz0123456789-_./:;=, "
+    n = 1 << 19
+    pieces = [oracle_mod.write_string(bytes(rng.choice(alpha) for _ in range(rng.randint(0, 40))), prefix=7,
+                                      choice=rng.choice([1, 1, 1, 2])) for _ in range(4096)]
+    blk, pos = bytearray(), []
+    for _ in range(n):
+        pos.append(len(blk))
+        blk += pieces[rng.randrange(len(pieces))]
+    blk = bytes(blk)
+    if order == "runs":
+        runs = [pos[k:k + 300] for k in range(0, n, 300)]
+        rng.shuffle(runs)
+        pos = [p for r in runs for p in r]
+    ref_vals, ref_st, ref_nxt = codec.read_strings(blk, pos, [7] * n)
+    L = len(blk)
+    dev = torch.device("cuda:0")
+    t_blk = torch.frombuffer(bytearray(blk), dtype=torch.uint8).to(dev)
+    t_pos = torch.tensor(np.asarray(pos, dtype=np.int64), device=dev)
+    t_lim = torch.full((n,), L, dtype=torch.int64, device=dev)
+    t_pf = torch.full((n,), 7, dtype=torch.uint8, device=dev)
+    out = torch.full((L * 8 // 5 + 16,), 0xA5, dtype=torch.uint8, device=dev)
+    out_off = torch.full((n + 1,), -1, dtype=torch.int64, device=dev)
+    out_len = torch.full((n,), -1, dtype=torch.int32, device=dev)
+    st = torch.full((n,), 0xEE, dtype=torch.uint8, device=dev)
+    nxt = torch.full((n,), -1, dtype=torch.int64, device=dev)
+    monkeypatch.setenv("MHQ_DEBUG_POISON_SCRATCH", "1")
+    codec.read_strings_dev(t_blk, t_pos, t_lim, t_pf, out, out_off, out_len, st, nxt)
+    torch.cuda.synchronize()
+    monkeypatch.delenv("MHQ_DEBUG_POISON_SCRATCH")
+    oo = out_off.cpu().numpy().view(np.uint64)
+    ol = out_len.cpu().numpy().view(np.uint32)
+    assert (st.cpu().numpy() == np.asarray(ref_st)).all()
+    assert (nxt.cpu().numpy().view(np.uint64) == np.asarray(ref_nxt)).all()
+    assert (ol == np.asarray([len(v) for v in ref_vals], dtype=np.uint32)).all()
+    assert int(oo[n]) <= out.numel() and (np.diff(oo.astype(np.int64)) >= 0).all()
+    o = out.cpu().numpy()
+    assert all(o[int(oo[k]): int(oo[k]) + int(ol[k])].tobytes() == ref_vals[k] for k in range(n))
+    for i in sorted(rng.sample(range(n), 5000)):
+        ref, rc, used = oracle_mod.read_string(blk[pos[i]:pos[i] + 200], prefix=7)
+        assert (ref_vals[i], int(ref_st[i])) == (ref, _oracle_status(rc)), i
+        assert int(ref_nxt[i]) == pos[i] + used
