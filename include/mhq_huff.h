@@ -85,7 +85,9 @@ int mhq_huff_encode_len(mhq_ctx *ctx, const uint8_t *in, const uint64_t *in_off,
 
 /* HuffmanCompressor.Write + Pad per literal (hc/huffman.go:23-37): codes
  * MSB-first, final octet padded with 1 bits.  out_off[i+1]-out_off[i] must be
- * at least enc_len[i]; bytes past enc_len[i] in a region are unspecified.  An
+ * at least enc_len[i]; bytes past enc_len[i] in a region are unspecified (the
+ * host forms: zero when the call stages through device buffers, the caller's
+ * old contents when it runs in place on pinned buffers).  An
  * empty region (out_off[i+1] == out_off[i]) skips literal i: nothing of it is
  * written (a caller encoding a subset places only that subset). */
 int mhq_huff_encode(mhq_ctx *ctx, const uint8_t *in, const uint64_t *in_off, uint64_t n, uint8_t *out,
@@ -95,7 +97,10 @@ int mhq_huff_encode(mhq_ctx *ctx, const uint8_t *in, const uint64_t *in_off, uin
  * into a region of capacity out_off[i+1]-out_off[i] (floor(8*len/5) always
  * suffices; hc/io.go:87 allocates len*8/5+1).  Writes out_len[i] and
  * status[i].  Trailing partial codes (padding) are dropped without checks,
- * as in the reference.  Bytes past out_len[i] in a region are unspecified. */
+ * as in the reference.  Bytes past out_len[i] in a region are unspecified:
+ * zero when the call stages through device buffers (pageable memory), the
+ * caller's old contents when it runs in place on pinned buffers; compare
+ * out_len[i] bytes only. */
 int mhq_huff_decode(mhq_ctx *ctx, const uint8_t *in, const uint64_t *in_off, uint64_t n, uint8_t *out,
                     const uint64_t *out_off, uint32_t *out_len, uint8_t *status);
 

@@ -327,16 +327,15 @@ int run_chunk(Device *d, Stage &S, const HostJob &j, uint64_t a, uint64_t b) {
   const uint64_t out_bias = j.out_off[a];
   const uint64_t out_bytes = j.out_off[b] - j.out_off[a];
   MHQ_TRY(hipMemcpyAsync(S.out_off.p, j.out_off + a, (m + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, s));
-  // A decode's staging region is zeroed first: the region is copied back
-  // whole, and bytes the kernel leaves alone (past a literal's out_len on the
-  // decode's streamed path) would otherwise carry an earlier call's data into
-  // the caller's buffer.  The fill is in stream order, before the kernel (a
-  // few MB per chunk).  Encode needs none: both encode kernels write every
-  // byte of a region (host-path regions are exactly enc_len long).
+  // The staging region is zeroed first: it is copied back whole, and bytes
+  // the kernels leave alone -- past a literal's out_len (decode), past its
+  // enc_len in a region longer than that or of a literal the encode skips
+  // (mhq_huff.h lets a region be longer) -- would otherwise carry an earlier
+  // call's data, perhaps another request's headers, into the caller's
+  // buffer.  The fill is in stream order, before the kernel (a few MB per
+  // chunk, beside its PCIe copies).
   uint8_t *dout = (uint8_t *)S.out.p;
-#ifndef MHQ_X_NOMEMSET  // (host-path experiment only: bytes past out_len left as they were)
-  if (j.op == Op::kDecode) MHQ_TRY(hipMemsetAsync(dout, 0, out_bytes, s));
-#endif
+  MHQ_TRY(hipMemsetAsync(dout, 0, out_bytes, s));
   const uint64_t *dout_off = (const uint64_t *)S.out_off.p;
   if (j.op == Op::kEncode) {
     MHQ_TRY(mhq::launch_encode(d->tables, din, din_off, in_bias, m, dout, dout_off, out_bias, s));

@@ -431,6 +431,45 @@ def test_encode_empty_region_skips_literal(codec, oracle_mod):
     assert (got[int(oo[-1]):] == 0xAB).all()
 
 
+def test_host_encode_oversized_regions_gap_bytes(codec, oracle_mod):
+    """mhq_huff_encode on pageable buffers (the staged route) into regions
+    longer than enc_len, some empty (the literal skipped): the encodings land
+    bit-exactly, and every other byte of the copied-back regions is zero --
+    never an earlier call's data from the reused device staging buffers
+    (the staged encode once skipped zeroing them)."""
+    import ctypes as C
+
+    from minhq_amd import hc, workloads
+
+    b = workloads.make_batch(40000, "uniform", "hdr", 12, 8, 64)
+    # an earlier call leaves plaintext in the staging buffers
+    enc0, eoff0 = codec.encode(b.data, b.off)
+    codec.decode(enc0, eoff0)
+    lits = hc.unpack(b.data, b.off)
+    rng = np.random.default_rng(5)
+    enc_len = np.array([len(oracle_mod.encode(x)) for x in lits], dtype=np.uint64)
+    keep = rng.random(len(lits)) < 0.9
+    extra = rng.integers(0, 24, len(lits)).astype(np.uint64)
+    region = np.where(keep, enc_len + extra, 0).astype(np.uint64)
+    oo = np.zeros(len(lits) + 1, dtype=np.uint64)
+    oo[1:] = np.cumsum(region)
+    out = np.full(int(oo[-1]) + 1, 0x5A, dtype=np.uint8)
+    data = np.ascontiguousarray(b.data, dtype=np.uint8)
+    off = np.ascontiguousarray(b.off, dtype=np.uint64)
+    rc = codec._L.mhq_huff_encode(codec.handle, data.ctypes.data_as(C.POINTER(C.c_uint8)),
+                                  off.ctypes.data_as(C.POINTER(C.c_uint64)), len(lits),
+                                  out.ctypes.data_as(C.POINTER(C.c_uint8)), oo.ctypes.data_as(C.POINTER(C.c_uint64)))
+    assert rc == 0
+    for i in range(len(lits)):
+        a, r = int(oo[i]), int(region[i])
+        if not r:
+            continue
+        e = int(enc_len[i])
+        assert out[a:a + e].tobytes() == oracle_mod.encode(lits[i]), i
+        assert (out[a + e:a + r] == 0).all(), i
+    assert out[-1] == 0x5A
+
+
 class _Pinned:
     """Allocator of pinned (page-locked) host buffers for the host entry
     points: with every buffer pinned the kernels read and write them in place
