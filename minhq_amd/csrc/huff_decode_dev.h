@@ -521,23 +521,46 @@ __device__ __forceinline__ uint64_t uniform64(uint64_t v) {
 
 // Offsets of the tile that starts at literal s (indices clamped to L1, so a
 // tile past the range loads the range end).
+// Indices relative to the tile's clamped start (a uniform base: the loads
+// take a scalar base and a 32-bit lane offset, no 64-bit index arithmetic per
+// lane); every workgroup range is under 2^32 literals.
+struct TileIdx {
+  uint64_t base;    // min(s, L1)
+  uint32_t a0, a1;  // literals s + 2 lane + {0, 1}, clamped to L1
+  uint32_t ae;      // literal s + tile, clamped to L1 (a vector index: see vzero)
+  __device__ __forceinline__ TileIdx(uint64_t s, uint64_t L1, uint32_t tl, uint32_t lane) {
+    base = min(s, L1);
+    const uint32_t lim = (uint32_t)(L1 - base);
+    a0 = min(2u * lane, lim);
+    a1 = min(2u * lane + 1u, lim);
+    ae = min(tl, lim) + vzero();  // keeps the uniform load a per-lane vector load
+  }
+};
+// (in_end has n entries: indices clamped below L1, i.e. in_end[min(s + j, L1 - 1)])
+template <bool kGaps>
+__device__ __forceinline__ void load_end(TileOff &t, const uint32_t *__restrict__ in_end, uint64_t s, uint64_t L1,
+                                         uint32_t lane) {
+  if (!kGaps) return;
+  const uint64_t eb = min(s, L1 - 1u);
+  const uint32_t elim = (uint32_t)(L1 - 1u - eb);
+  const uint32_t *e = in_end + eb;
+  t.e0 = e[min(2u * lane, elim)];
+  t.e1 = e[min(2u * lane + 1u, elim)];
+}
+
 template <bool kGaps>
 __device__ __forceinline__ void load_off(TileOff &t, const uint64_t *__restrict__ in_off,
                                          const uint32_t *__restrict__ in_end, const uint64_t *__restrict__ out_off,
                                          uint64_t s, uint64_t L1, uint32_t tl, uint32_t lane) {
-  const uint32_t z = vzero();  // keeps the loads per-lane vector loads
-  const uint64_t j0 = min(s + 2u * lane, L1) + z, j1 = min(s + 2u * lane + 1u, L1) + z;
-  const uint64_t je = min(s + (uint64_t)tl, L1) + z;
-  t.i0 = in_off[j0];
-  t.i1 = lo32(in_off, j1);
-  if (kGaps) {  // (in_end has n entries: indices clamped below L1)
-    t.e0 = in_end[min(j0, L1 - 1u)];
-    t.e1 = in_end[min(j1, L1 - 1u)];
-  }
-  t.o0 = out_off[j0];
-  t.o1 = lo32(out_off, j1);
-  t.ie = in_off[je];
-  t.oe = out_off[je];
+  const TileIdx x(s, L1, tl, lane);
+  const uint64_t *ib = in_off + x.base, *ob = out_off + x.base;
+  t.i0 = ib[x.a0];
+  t.i1 = lo32(ib, x.a1);
+  load_end<kGaps>(t, in_end, s, L1, lane);
+  t.o0 = ob[x.a0];
+  t.o1 = lo32(ob, x.a1);
+  t.ie = ib[x.ae];
+  t.oe = ob[x.ae];
 }
 
 // The two halves of load_off, for the launch's opening.
@@ -545,25 +568,20 @@ template <bool kGaps>
 __device__ __forceinline__ void load_off_in(TileOff &t, const uint64_t *__restrict__ in_off,
                                             const uint32_t *__restrict__ in_end, uint64_t s, uint64_t L1,
                                             uint32_t tl, uint32_t lane) {
-  const uint32_t z = vzero();
-  const uint64_t j0 = min(s + 2u * lane, L1) + z, j1 = min(s + 2u * lane + 1u, L1) + z;
-  const uint64_t je = min(s + (uint64_t)tl, L1) + z;
-  t.i0 = in_off[j0];
-  t.i1 = lo32(in_off, j1);
-  if (kGaps) {
-    t.e0 = in_end[min(j0, L1 - 1u)];
-    t.e1 = in_end[min(j1, L1 - 1u)];
-  }
-  t.ie = in_off[je];
+  const TileIdx x(s, L1, tl, lane);
+  const uint64_t *ib = in_off + x.base;
+  t.i0 = ib[x.a0];
+  t.i1 = lo32(ib, x.a1);
+  load_end<kGaps>(t, in_end, s, L1, lane);
+  t.ie = ib[x.ae];
 }
 __device__ __forceinline__ void load_off_out(TileOff &t, const uint64_t *__restrict__ out_off, uint64_t s,
                                              uint64_t L1, uint32_t tl, uint32_t lane) {
-  const uint32_t z = vzero();
-  const uint64_t j0 = min(s + 2u * lane, L1) + z, j1 = min(s + 2u * lane + 1u, L1) + z;
-  const uint64_t je = min(s + (uint64_t)tl, L1) + z;
-  t.o0 = out_off[j0];
-  t.o1 = lo32(out_off, j1);
-  t.oe = out_off[je];
+  const TileIdx x(s, L1, tl, lane);
+  const uint64_t *ob = out_off + x.base;
+  t.o0 = ob[x.a0];
+  t.o1 = lo32(ob, x.a1);
+  t.oe = ob[x.ae];
 }
 
 struct TileIn {
