@@ -123,6 +123,20 @@ int mhq_huff_offsets_dev(mhq_ctx *ctx, int dev, const uint32_t *enc_len, uint64_
 int mhq_huff_encode_layout_dev(mhq_ctx *ctx, int dev, const uint8_t *in, const uint64_t *in_off, uint64_t n,
                                uint64_t base, uint32_t *enc_len, uint64_t *out_off, uint64_t *cap_off,
                                void *stream);
+/* The encode side of a batch in one call: enc_len[i], out_off (from base,
+ * n+1 entries), cap_off (may be NULL) as mhq_huff_encode_layout_dev writes
+ * them, and the encodings as mhq_huff_encode_dev writes them, literal i at
+ * out[out_off[i] - base].  in_bytes must be in_off[n] - in_off[0]; out_cap (out's
+ * size) must be at least (30 * in_bytes + 7) / 8, the most any plaintext
+ * encodes to (MHQ_EINVAL otherwise).  A batch of short literals (mean up to
+ * 40 bytes, under 2^29 bytes) takes ONE launch that stages each range of
+ * literals once: sized, placed by a look-back over the ranges before it,
+ * encoded (enc_packed.hip); other batches take the layout call and the
+ * encode.  Replaces hc/io.go:157-172's sizing and hc/huffman.go:23-37's
+ * Write + Pad for a batch, plus the placement the caller would do. */
+int mhq_huff_encode_packed_dev(mhq_ctx *ctx, int dev, const uint8_t *in, const uint64_t *in_off, uint64_t n,
+                               uint64_t in_bytes, uint64_t base, uint32_t *enc_len, uint64_t *out_off,
+                               uint64_t *cap_off, uint8_t *out, uint64_t out_cap, void *stream);
 /* cap_off[i] = base + sum_{j<i} floor(8*(in_off[j+1]-in_off[j])/5). */
 int mhq_huff_capacity_dev(mhq_ctx *ctx, int dev, const uint64_t *in_off, uint64_t n, uint64_t base,
                           uint64_t *cap_off, void *stream);

@@ -54,6 +54,8 @@ SIGNATURES = {
     "mhq_huff_encode_len_dev": (C.c_int, [vp, C.c_int, vp, vp, C.c_uint64, vp, vp]),
     "mhq_huff_offsets_dev": (C.c_int, [vp, C.c_int, vp, C.c_uint64, C.c_uint64, vp, vp, vp]),
     "mhq_huff_encode_layout_dev": (C.c_int, [vp, C.c_int, vp, vp, C.c_uint64, C.c_uint64, vp, vp, vp, vp]),
+    "mhq_huff_encode_packed_dev": (C.c_int, [vp, C.c_int, vp, vp, C.c_uint64, C.c_uint64, C.c_uint64, vp, vp, vp,
+                                             vp, C.c_uint64, vp]),
     "mhq_huff_capacity_dev": (C.c_int, [vp, C.c_int, vp, C.c_uint64, C.c_uint64, vp, vp]),
     "mhq_huff_encode_dev": (C.c_int, [vp, C.c_int, vp, vp, C.c_uint64, vp, vp, vp]),
     "mhq_huff_decode_dev": (C.c_int, [vp, C.c_int, vp, vp, C.c_uint64, vp, vp, vp, vp, vp]),

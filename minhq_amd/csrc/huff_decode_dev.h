@@ -344,7 +344,7 @@ __device__ __forceinline__ bool win_step_w(const Smem &sm, WinBuf3 &in, uint32_t
 // [p, endbit), output at slice byte optr), stored again byte by byte: the
 // bytes a neighbour's end stores (win_step_w) clobbered.  The literal is
 // known to decode to at least cnt bytes.
-__device__ __noinline__ void repair_head(const Smem &sm, WaveSmem &ws, uint32_t p, uint32_t optr, uint32_t cnt) {
+[[maybe_unused]] __device__ __noinline__ void repair_head(const Smem &sm, WaveSmem &ws, uint32_t p, uint32_t optr, uint32_t cnt) {
   uint8_t *o = (uint8_t *)ws.out_w + optr;
   for (uint32_t k = 0; k < cnt;) {
     const uint32_t w0 = ws.in_w[p >> 5], w1 = ws.in_w[(p >> 5) + 1u];

@@ -35,6 +35,15 @@ hipError_t launch_offsets_sums(const uint32_t *enc_len, uint64_t n, uint64_t *bl
 hipError_t launch_encode(const DevTables &t, const uint8_t *in, const uint64_t *in_off,
                          uint64_t in_bias, uint64_t n, uint8_t *out, const uint64_t *out_off,
                          uint64_t out_bias, hipStream_t s);
+// encode_len + the offsets scan (out_off, cap_off from base) + encode in ONE
+// launch (enc_packed.hip), for batches under 2^29 plaintext bytes: out holds
+// the encodings from out_off[0] = base on, out_cap bytes (a literal whose
+// region ends past it is not written).  slots: encode_packed_slot_bytes(n)
+// bytes that only look-backs use (a stale slot carries another call's tag).
+size_t encode_packed_slot_bytes(uint64_t n);
+hipError_t launch_encode_packed(const DevTables &t, const uint8_t *in, const uint64_t *in_off, uint64_t in_bias,
+                                uint64_t n, uint64_t base, uint32_t *enc_len, uint64_t *out_off, uint64_t *cap_off,
+                                uint8_t *out, uint64_t out_cap, uint64_t *slots, uint64_t gen, hipStream_t s);
 // in_end (optional): literal i is in[in_off[i] - in_bias .. e_i - in_bias), e_i
 // the first position at or after in_off[i] whose low 32 bits are in_end[i]
 // (literals under 4 GiB); e_i <= in_off[i + 1] when the literals are in order

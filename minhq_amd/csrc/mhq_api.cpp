@@ -14,6 +14,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cstdio>
 #include <memory>
@@ -101,6 +102,10 @@ struct Device {
   };
   std::mutex scratch_mu;
   std::vector<Scratch> scratch;
+  // Look-back slots (mhq_huff_encode_packed_dev), one buffer per caller
+  // stream, written by nothing else: a stale slot holds an earlier call's
+  // tag, never another entry point's data.
+  std::vector<Scratch> slots;
   // Buffers a stream outgrew.  Work queued (possibly by another thread on the
   // same stream) may still use them: once the last caller holding one has
   // finished enqueueing (its ScratchLease ends) an event is recorded on the
@@ -178,6 +183,8 @@ void free_device(Device *d) {
   if (d->table_mem) (void)hipFree(d->table_mem);
   for (auto &x : d->scratch) (void)hipFree(x.p);
   d->scratch.clear();
+  for (auto &x : d->slots) (void)hipFree(x.p);
+  d->slots.clear();
   for (auto &r : d->retired) {
     (void)hipFree(r.p);
     if (r.done) (void)hipEventDestroy(r.done);
@@ -221,10 +228,10 @@ void reap_retired(Device *d) {
 // new one and the old one retired (freed by reap_retired once its stream has
 // passed it): another thread may have just been handed it for work it is
 // still queueing on the same stream.
-void *stream_scratch(Device *d, hipStream_t s, size_t bytes) {
+void *stream_buffer(Device *d, std::vector<Device::Scratch> &pool, hipStream_t s, size_t bytes) {
   std::lock_guard<std::mutex> g(d->scratch_mu);
   reap_retired(d);
-  for (auto &x : d->scratch) {
+  for (auto &x : pool) {
     if (x.s != s) continue;
     if (x.bytes >= bytes) {
       x.holders++;
@@ -241,25 +248,27 @@ void *stream_scratch(Device *d, hipStream_t s, size_t bytes) {
     x.holders = 1;
     return x.p;
   }
-  if (d->scratch.size() >= kMaxScratchStreams) return nullptr;
+  if (pool.size() >= kMaxScratchStreams) return nullptr;
   size_t b = 65536;
   while (b < bytes) b <<= 1;
   void *p = nullptr;
   if (hipMalloc(&p, b) != hipSuccess) return nullptr;
-  d->scratch.push_back(Device::Scratch{s, p, b, 1});
+  pool.push_back(Device::Scratch{s, p, b, 1});
   return p;
 }
+void *stream_scratch(Device *d, hipStream_t s, size_t bytes) { return stream_buffer(d, d->scratch, s, bytes); }
 
 // Ends a caller's hold on a buffer from stream_scratch (after it has
 // enqueued every use of it).
 void release_scratch(Device *d, void *p) {
   if (!p) return;
   std::lock_guard<std::mutex> g(d->scratch_mu);
-  for (auto &x : d->scratch)
-    if (x.p == p) {
-      x.holders--;
-      return;
-    }
+  for (auto *pool : {&d->scratch, &d->slots})
+    for (auto &x : *pool)
+      if (x.p == p) {
+        x.holders--;
+        return;
+      }
   for (auto &r : d->retired)
     if (r.p == p) {
       r.holders--;
@@ -274,6 +283,8 @@ struct ScratchLease {
   Device *d;
   void *p;
   ScratchLease(Device *d_, hipStream_t s, size_t bytes) : d(d_), p(bytes ? stream_scratch(d_, s, bytes) : nullptr) {}
+  ScratchLease(Device *d_, std::vector<Device::Scratch> &pool, hipStream_t s, size_t bytes)
+      : d(d_), p(bytes ? stream_buffer(d_, pool, s, bytes) : nullptr) {}
   ~ScratchLease() { release_scratch(d, p); }
   ScratchLease(const ScratchLease &) = delete;
   ScratchLease &operator=(const ScratchLease &) = delete;
@@ -636,6 +647,32 @@ int mhq_huff_encode_layout_dev(mhq_ctx *ctx, int dev, const uint8_t *in, const u
   if (e == hipSuccess) e = mhq::launch_offsets_sums(enc_len, n, sums, base, out_off, cap_off, s);
   const hipError_t e2 = own ? hipFreeAsync(sums, s) : hipSuccess;
   return hip_rc(e != hipSuccess ? e : e2);
+}
+
+int mhq_huff_encode_packed_dev(mhq_ctx *ctx, int dev, const uint8_t *in, const uint64_t *in_off, uint64_t n,
+                               uint64_t in_bytes, uint64_t base, uint32_t *enc_len, uint64_t *out_off,
+                               uint64_t *cap_off, uint8_t *out, uint64_t out_cap, void *stream) {
+  Device *d = device(ctx, dev);
+  if (!d || !out_off || (n && (!in_off || !enc_len || !out))) return MHQ_EINVAL;
+  if (in_bytes > (UINT64_MAX - 7) / 30 || out_cap < (30 * in_bytes + 7) / 8) return MHQ_EINVAL;
+  MHQ_TRY(hipSetDevice(d->ordinal));
+  hipStream_t s = (hipStream_t)stream;
+  // one launch for short literals (the thread form's band, mean <= 40 B, and
+  // every look-back sum under 2^32); otherwise the layout call and the
+  // encode, whose forms suit long literals
+  if (in_bytes < ((uint64_t)1 << 29) && in_bytes <= 40 * n) {
+    ScratchLease slots(d, d->slots, s, mhq::encode_packed_slot_bytes(n));
+    if (slots.p) {
+      static std::atomic<uint64_t> g_gen{0};
+      const uint64_t gen = g_gen.fetch_add(1, std::memory_order_relaxed) + 1;
+      return hip_rc(mhq::launch_encode_packed(d->tables, in, in_off, 0, n, base, enc_len, out_off, cap_off, out,
+                                              out_cap, (uint64_t *)slots.p, gen, s));
+    }
+  }
+  const int rc = mhq_huff_encode_layout_dev(ctx, dev, in, in_off, n, base, enc_len, out_off, cap_off, stream);
+  if (rc != MHQ_OK || n == 0) return rc;
+  // (launch_encode places literal i at out_off[i] - base from `out`)
+  return hip_rc(mhq::launch_encode(d->tables, in, in_off, 0, n, out, out_off, base, s));
 }
 
 int mhq_huff_capacity_dev(mhq_ctx *ctx, int dev, const uint64_t *in_off, uint64_t n, uint64_t base,

@@ -372,6 +372,17 @@ class Codec:
                                                  cap_off.data_ptr() if cap_off is not None else None,
                                                  self._stream(stream)), "encode_layout_dev")
 
+    def encode_packed_dev(self, data, off, in_bytes: int, enc_len, out_off, cap_off, out, base: int = 0,
+                          dev: int = 0, stream=None) -> None:
+        """encode_layout_dev + encode_dev in one call (one launch for short
+        literals); out must hold (30 * in_bytes + 7) // 8 bytes."""
+        n = off.numel() - 1
+        check(self._L.mhq_huff_encode_packed_dev(self._h, dev, data.data_ptr(), off.data_ptr(), n, in_bytes, base,
+                                                 enc_len.data_ptr(), out_off.data_ptr(),
+                                                 cap_off.data_ptr() if cap_off is not None else None,
+                                                 out.data_ptr(), out.numel(), self._stream(stream)),
+              "encode_packed_dev")
+
     def capacity_dev(self, in_off, cap_off, base: int = 0, dev: int = 0, stream=None) -> None:
         n = in_off.numel() - 1
         check(self._L.mhq_huff_capacity_dev(self._h, dev, in_off.data_ptr(), n, base, cap_off.data_ptr(),

@@ -1,0 +1,149 @@
+"""mhq_huff_encode_packed_dev: the encode side of a batch in one call (one
+launch for short literals, enc_packed.hip) against the oracle -- enc_len,
+out_off, cap_off and every encoded byte -- on the shapes that reach each of
+its paths: staged ranges, ranges too long to stage (a long literal among short
+ones), output too long for the staging slice, empty literals, partial last
+ranges, grids far larger than one resident generation (look-back windows
+over many predecessors), a base offset, no cap_off, and batches of longer
+literals (the layout + encode path).  Reference: hc/huffman.go:23-37,
+hc/io.go:157-172."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def codec():
+    from minhq_amd import build, hc
+
+    build.build()
+    c = hc.Codec(1)
+    yield c
+    c.close()
+
+
+def _run(codec, oracle_mod, data, off, base=0, with_cap=True, stream=None):
+    import torch
+
+    dev = torch.device("cuda:0")
+    n = len(off) - 1
+    in_bytes = int(off[-1] - off[0])
+    t_data = torch.from_numpy(np.ascontiguousarray(data, dtype=np.uint8).copy()).to(dev)
+    if t_data.numel() == 0:
+        t_data = torch.zeros(1, dtype=torch.uint8, device=dev)
+    t_off = torch.from_numpy(off.astype(np.uint64).view(np.int64).copy()).to(dev)
+    enc_len = torch.full((max(n, 1),), -1, dtype=torch.int32, device=dev)
+    out_off = torch.full((n + 1,), -1, dtype=torch.int64, device=dev)
+    cap_off = torch.full((n + 1,), -1, dtype=torch.int64, device=dev) if with_cap else None
+    cap = (30 * in_bytes + 7) // 8
+    out = torch.full((max(cap, 1),), 0xA5, dtype=torch.uint8, device=dev)
+    torch.cuda.synchronize()  # (the inputs' copies are on the current stream)
+    codec.encode_packed_dev(t_data, t_off, in_bytes, enc_len, out_off, cap_off, out, base=base, stream=stream)
+    torch.cuda.synchronize()
+    ref_len = oracle_mod.encode_len_batch(data, off, nthreads=8) if n else np.zeros(0, np.uint32)
+    eoff = np.zeros(n + 1, dtype=np.uint64)
+    eoff[1:] = np.cumsum(ref_len, dtype=np.uint64)
+    coff = np.zeros(n + 1, dtype=np.uint64)
+    coff[1:] = np.cumsum(ref_len.astype(np.uint64) * 8 // 5, dtype=np.uint64)
+    ref_enc = oracle_mod.encode_batch(data, off, eoff, nthreads=8) if n else np.zeros(0, np.uint8)
+    assert np.array_equal(enc_len.cpu().numpy()[:n].view(np.uint32), ref_len)
+    assert np.array_equal(out_off.cpu().numpy().view(np.uint64), eoff + base)
+    if with_cap:
+        assert np.array_equal(cap_off.cpu().numpy().view(np.uint64), coff + base)
+    got = out.cpu().numpy()
+    assert got[: int(eoff[-1])].tobytes() == ref_enc.tobytes()
+
+
+@pytest.mark.parametrize("shape", ["northstar", "config2", "print", "qif_short", "odd_n"])
+def test_packed_short_shapes(codec, oracle_mod, shape):
+    from minhq_amd import workloads as w
+
+    if shape == "northstar":
+        b = w.north_star(1 << 17)
+    elif shape == "config2":
+        b = w.config2(1 << 17)
+    elif shape == "print":
+        b = w.config2(1 << 16, "print")
+    elif shape == "qif_short":
+        b = w.make_batch(50000, "uniform", "hdr", 41, 0, 26)
+    else:
+        b = w.make_batch(512 * 37 + 311, "uniform", "hdr", 42, 0, 70)
+    _run(codec, oracle_mod, b.data, b.off)
+
+
+def test_packed_many_ranges_base_no_cap(codec, oracle_mod):
+    """2^20 literals: 2048 ranges, far more than one resident generation, so
+    look-backs cross windows of 512 predecessors; a base offset; no cap_off."""
+    from minhq_amd import workloads as w
+
+    b = w.north_star(1 << 20)
+    _run(codec, oracle_mod, b.data, b.off, base=12345, with_cap=False)
+
+
+def test_packed_unstaged_ranges(codec, oracle_mod):
+    """Ranges whose plaintext exceeds the 24 KiB staging slice (a 3 KB
+    literal every 700, a 40 KB one once) or whose output exceeds the 20 KiB
+    output slice (random bytes: 30-bit codes), sized and encoded per literal
+    from global memory; empty literals throughout."""
+    from minhq_amd import hc, workloads as w
+
+    rng = np.random.default_rng(43)
+    b = w.make_batch(30000, "uniform", "hdr", 43, 0, 40)
+    lits = hc.unpack(b.data, b.off)
+    for i in range(0, len(lits), 700):
+        lits[i] = bytes(rng.integers(32, 127, 3000, dtype=np.uint8))
+    lits[12000] = bytes(rng.integers(0, 256, 40000, dtype=np.uint8))
+    for i in range(25000, 25512):  # one range of random bytes: ~3.7x expansion, its output over the slice
+        lits[i] = bytes(rng.integers(0, 256, 40, dtype=np.uint8))
+    for i in range(5, len(lits), 97):
+        lits[i] = b""
+    data, off = hc.pack(lits)
+    _run(codec, oracle_mod, data, off)
+
+
+def test_packed_long_literals_path(codec, oracle_mod):
+    """Mean literal over 40 bytes: the layout call and the encode, same results."""
+    from minhq_amd import workloads as w
+
+    b = w.make_batch(20000, "uniform", "hdr", 44, 30, 200)
+    _run(codec, oracle_mod, b.data, b.off, base=7)
+
+
+def test_packed_tiny_batches(codec, oracle_mod):
+    from minhq_amd import hc
+
+    _run(codec, oracle_mod, np.zeros(0, np.uint8), np.zeros(1, np.uint64), base=3)
+    for lits in ([b""], [b"a"], [b"", b"", b""], [bytes(range(256))], [b"www.example.com"] * 513):
+        data, off = hc.pack(lits)
+        _run(codec, oracle_mod, data, off)
+
+
+def test_packed_repeated_calls_two_streams(codec, oracle_mod):
+    """Calls back to back on one stream (the stream's look-back slots hold the
+    previous call's tags) and alternating over two streams."""
+    import torch
+
+    from minhq_amd import workloads as w
+
+    s2 = torch.cuda.Stream()
+    for k in range(4):
+        b = w.north_star(100000 + 1000 * k)
+        _run(codec, oracle_mod, b.data, b.off, stream=None if k % 2 == 0 else s2.cuda_stream)
+
+
+def test_packed_rejects_small_out(codec):
+    import torch
+
+    from minhq_amd import _lib, workloads as w
+
+    b = w.north_star(1000)
+    dev = torch.device("cuda:0")
+    t_data = torch.from_numpy(b.data.copy()).to(dev)
+    t_off = torch.from_numpy(b.off.view(np.int64).copy()).to(dev)
+    in_bytes = int(b.off[-1])
+    enc_len = torch.empty(1000, dtype=torch.int32, device=dev)
+    out_off = torch.empty(1001, dtype=torch.int64, device=dev)
+    out = torch.empty((30 * in_bytes + 7) // 8 - 1, dtype=torch.uint8, device=dev)
+    with pytest.raises(_lib.MhqError):
+        codec.encode_packed_dev(t_data, t_off, in_bytes, enc_len, out_off, None, out)
