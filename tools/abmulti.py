@@ -44,7 +44,7 @@ def open_lib(path):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--kernel", default="decode", choices=["decode", "encode", "layout"])
+    ap.add_argument("--kernel", default="decode", choices=["decode", "encode", "layout", "packed", "layenc"])
     ap.add_argument("--configs", default="northstar")
     ap.add_argument("--libs", required=True)
     ap.add_argument("--reps", type=int, default=3)
@@ -91,6 +91,9 @@ def main():
         elif args.kernel == "encode":
             per = b.nbytes + enc_bytes + 16 * n
             alg = b.nbytes + enc_bytes + 16 * (n + 1) + 4 * n
+        elif args.kernel in ("packed", "layenc"):  # the encode side: plaintext in, lengths, offsets, codes out
+            per = b.nbytes + (30 * b.nbytes + 7) // 8 + 32 * n
+            alg = b.nbytes + enc_bytes + 8 * (n + 1) + 4 * n + 8 * (n + 1) + 8 * (n + 1)
         else:
             per = b.nbytes + 32 * n
             alg = b.nbytes + 8 * (n + 1) + 8 * n + 16 * (n + 1)
@@ -106,7 +109,7 @@ def main():
             else:
                 s["in"], s["off"] = data.clone(), off.clone()
                 s["eoff"] = enc_off.clone()
-                s["out"] = torch.empty(enc_bytes + 16, dtype=torch.uint8, device=dev)
+                s["out"] = torch.empty(max(enc_bytes + 16, (30 * b.nbytes + 7) // 8), dtype=torch.uint8, device=dev)
                 s["len"] = torch.empty(n, dtype=torch.int32, device=dev)
                 s["o1"] = torch.empty_like(enc_off)
                 s["o2"] = torch.empty_like(cap_off)
@@ -119,10 +122,17 @@ def main():
             elif args.kernel == "encode":
                 rc = L.mhq_huff_encode_dev(h, 0, s["in"].data_ptr(), s["off"].data_ptr(), n, s["out"].data_ptr(),
                                            s["eoff"].data_ptr(), stream)
+            elif args.kernel == "packed":
+                rc = L.mhq_huff_encode_packed_dev(h, 0, s["in"].data_ptr(), s["off"].data_ptr(), n, b.nbytes, 0,
+                                                  s["len"].data_ptr(), s["o1"].data_ptr(), s["o2"].data_ptr(),
+                                                  s["out"].data_ptr(), s["out"].numel(), stream)
             else:
                 rc = L.mhq_huff_encode_layout_dev(h, 0, s["in"].data_ptr(), s["off"].data_ptr(), n, 0,
                                                   s["len"].data_ptr(), s["o1"].data_ptr(), s["o2"].data_ptr(),
                                                   stream)
+                if rc == 0 and args.kernel == "layenc":
+                    rc = L.mhq_huff_encode_dev(h, 0, s["in"].data_ptr(), s["off"].data_ptr(), n, s["out"].data_ptr(),
+                                               s["o1"].data_ptr(), stream)
             if rc != 0:
                 raise RuntimeError(f"rc={rc}")
 

@@ -15,3 +15,8 @@ timeout -k 10 600 python3 tools/abmulti.py --kernel decode --configs northstar,c
   --libs base=minhq_amd/libmhq_huff.so,bw=build/v/lib_bw.so,bw4=build/v/lib_bw4.so --check bw,bw4 --reps 3 \
   > "$OUT/ab_bw.txt" 2>&1 || { echo "ab failed"; tail -20 "$OUT/ab_bw.txt"; exit 1; }
 cat "$OUT/ab_bw.txt"
+timeout -k 10 600 python3 tools/abmulti.py --kernel layenc --configs northstar,config2,config3 \
+  --libs base=minhq_amd/libmhq_huff.so > "$OUT/ab_layenc.txt" 2>&1 && \
+timeout -k 10 600 python3 tools/abmulti.py --kernel packed --configs northstar,config2,config3 \
+  --libs base=minhq_amd/libmhq_huff.so > "$OUT/ab_packed.txt" 2>&1 || { echo "packed ab failed"; tail -20 "$OUT/ab_packed.txt"; exit 1; }
+cat "$OUT/ab_layenc.txt" "$OUT/ab_packed.txt"
