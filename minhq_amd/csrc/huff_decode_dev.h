@@ -87,6 +87,29 @@ __device__ __noinline__ void dbg_fail(uint32_t code, uint64_t a, uint64_t b) {
   do {                                                                   \
     if (!(c)) dbg_fail((code), (uint64_t)(a), (uint64_t)(b));            \
   } while (0)
+// Guards (the same build): an access whose address fails its check is
+// recorded and SKIPPED, so a bad address shows up as a record instead of a
+// fault.  g_dbg_mem: the global byte ranges the read path may write (the
+// output) and read (the block), set by the read launchers (0: unchecked).
+__device__ uint64_t g_dbg_mem[4];
+__device__ __forceinline__ bool dbg_out_ok(const void *p, uint64_t bytes) {
+  const uint64_t a = (uint64_t)(uintptr_t)p;
+  return g_dbg_mem[1] == 0 || (a >= g_dbg_mem[0] && a + bytes <= g_dbg_mem[1]);
+}
+__device__ __forceinline__ bool dbg_in_ok(const void *p, uint64_t bytes) {
+  const uint64_t a = (uint64_t)(uintptr_t)p;
+  return g_dbg_mem[3] == 0 || (a >= g_dbg_mem[2] && a + bytes <= g_dbg_mem[3]);
+}
+// an LDS address (generic or local) inside the decode's allocation
+__device__ __forceinline__ bool dbg_lds_ok(const void *p, uint64_t bytes) {
+  return (uint32_t)(uintptr_t)p + bytes <= 163840u;
+}
+#define DBG_OK(c, code, a, b) ((c) || (dbg_fail((code), (uint64_t)(a), (uint64_t)(b)), false))
+#define MHQ_DBG_SET_MEM(out_lo, out_hi, in_lo, in_hi)                                          \
+  do {                                                                                       \
+    const uint64_t _m[4] = {(uint64_t)(out_lo), (uint64_t)(out_hi), (uint64_t)(in_lo), (uint64_t)(in_hi)}; \
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_dbg_mem), _m, sizeof(_m));                          \
+  } while (0)
 #define MHQ_DBG_READER(name)                                                                  \
   extern "C" int name(unsigned long long *out, int n) {                                       \
     unsigned long long h[1 + 3 * 16];                                                         \
@@ -98,6 +121,10 @@ __device__ __noinline__ void dbg_fail(uint32_t code, uint64_t a, uint64_t b) {
 #else
 #define DBG_CHECK(c, code, a, b) \
   do {                           \
+  } while (0)
+#define DBG_OK(c, code, a, b) true
+#define MHQ_DBG_SET_MEM(out_lo, out_hi, in_lo, in_hi) \
+  do {                                                \
   } while (0)
 #endif
 
@@ -128,8 +155,9 @@ __device__ void decode_literal_global(const uint8_t *src, uint64_t nbytes, uint8
     const uint64_t rem = endbit - p;
     const uint64_t k = p >> 5;
     const uint32_t s = (uint32_t)p & 31u;
-    const uint32_t w0 = __builtin_bswap32(wb[k < lastw ? k : lastw]);
-    const uint32_t w1 = __builtin_bswap32(wb[k + 1 < lastw ? k + 1 : lastw]);
+    const uint32_t *r0 = wb + (k < lastw ? k : lastw), *r1 = wb + (k + 1 < lastw ? k + 1 : lastw);
+    const uint32_t w0 = DBG_OK(dbg_in_ok(r0, 4), 20, r0, src) ? __builtin_bswap32(*r0) : 0u;
+    const uint32_t w1 = DBG_OK(dbg_in_ok(r1, 4), 20, r1, src) ? __builtin_bswap32(*r1) : 0u;
     const uint32_t win = s ? (w0 << s) | (w1 >> (32u - s)) : w0;
     const uint32_t e = sm.lut1[win >> (32 - kLut1Bits)];
     if (e == 0) {  // a long code or the EOS prefix
@@ -142,15 +170,18 @@ __device__ void decode_literal_global(const uint8_t *src, uint64_t nbytes, uint8
       uint32_t sym = 0;
       const uint32_t L = long_code(sm.lut2, win, sym);
       if (L == 0 || L > rem) break;
-      dst[n++] = (uint8_t)sym;
+      if (DBG_OK(dbg_out_ok(dst + n, 1), 21, dst + n, cap)) dst[n] = (uint8_t)sym;
+      n++;
       p += L;
       continue;
     }
     const uint32_t tot = e & 0xffu, s0 = (e >> 16) & 0xffu, len0 = sm.clen[s0];
     if (len0 > rem) break;
-    dst[n++] = (uint8_t)s0;
+    if (DBG_OK(dbg_out_ok(dst + n, 1), 21, dst + n, cap)) dst[n] = (uint8_t)s0;
+    n++;
     if (((e >> 8) & 0xffu) == 16u && tot <= rem && n < cap) {
-      dst[n++] = (uint8_t)(e >> 24);
+      if (DBG_OK(dbg_out_ok(dst + n, 1), 21, dst + n, cap)) dst[n] = (uint8_t)(e >> 24);
+      n++;
       p += tot;
     } else {
       p += len0;
@@ -347,6 +378,7 @@ __device__ __forceinline__ bool win_step_w(const Smem &sm, WinBuf3 &in, uint32_t
 [[maybe_unused]] __device__ __noinline__ void repair_head(const Smem &sm, WaveSmem &ws, uint32_t p, uint32_t optr, uint32_t cnt) {
   uint8_t *o = (uint8_t *)ws.out_w + optr;
   for (uint32_t k = 0; k < cnt;) {
+    if (!DBG_OK(dbg_lds_ok(o + k, 2) && dbg_lds_ok(ws.in_w + (p >> 5), 8), 32, optr + k, p)) break;
     const uint32_t w0 = ws.in_w[p >> 5], w1 = ws.in_w[(p >> 5) + 1u];
     const uint32_t S = (p & 31u) ? (w0 << (p & 31u)) | (w1 >> (32u - (p & 31u))) : w0;
     const uint32_t e = sm.lut1[S >> (32 - kLut1Bits)];
@@ -373,7 +405,9 @@ struct BitBufS {
   uint64_t bb;
   uint32_t p, kb, w, swz;
   const uint32_t *in_w;
-  __device__ __forceinline__ uint32_t rd(const uint32_t *q, uint32_t k) const { return __builtin_bswap32(q[k ^ swz]); }
+  __device__ __forceinline__ uint32_t rd(const uint32_t *q, uint32_t k) const {
+    return DBG_OK(dbg_lds_ok(q + (k ^ swz), 4), 28, (uintptr_t)(q + (k ^ swz)), k) ? __builtin_bswap32(q[k ^ swz]) : 0u;
+  }
   __device__ __forceinline__ void init(const uint32_t *words, uint32_t p0, uint32_t swz_) {
     swz = swz_;
     in_w = words;
@@ -431,6 +465,7 @@ __device__ __noinline__ uint32_t decode_checked(const Smem &sm, WaveSmem &ws, ui
     in.p += cons;
     fin = c8 == 0;
     DBG_CHECK(out.ow < (uint32_t)kWOut / 4u + 4u, 5, out.ow, oend);
+    if (!DBG_OK(dbg_lds_ok(ws.out_w + out.ow, 4) && dbg_lds_ok(ws.in_w + (in.kb >> 5), 4), 22, out.ow, in.kb)) break;
     out.flush(ws.out_w);
   }
   const uint32_t oend_got = out.optr();
@@ -927,14 +962,15 @@ struct OutAccG {
     const uint32_t v = (uint32_t)acc;
     if (full && ow >= owf) {
       if (!grouped(ow)) {
-        gout[ow] = v;
+        if (DBG_OK(dbg_out_ok(gout + ow, 4), 23, gout + ow, ow)) gout[ow] = v;
       } else {
         const uint32_t r = (ow + ga) & 3u;
         q0 = r == 0u ? v : q0;
         q1 = r == 1u ? v : q1;
         q2 = r == 2u ? v : q2;
         q3 = r == 3u ? v : q3;
-        if (r == 3u) *(u32x4 *)(gout + ow - 3u) = u32x4{q0, q1, q2, v};
+        if (r == 3u && DBG_OK(dbg_out_ok(gout + ow - 3u, 16), 24, gout + ow - 3u, ow))
+          *(u32x4 *)(gout + ow - 3u) = u32x4{q0, q1, q2, v};
       }
     }
     first = (full && ow < owf) ? v : first;
@@ -947,16 +983,21 @@ struct OutAccG {
     // whole words of the last, incomplete 16-B group
     if (grouped(ow)) {
       const uint32_t r = (ow + ga) & 3u, g = ow - r;
-      if (r > 0u) gout[g] = q0;
-      if (r > 1u) gout[g + 1u] = q1;
-      if (r > 2u) gout[g + 2u] = q2;
+      if (DBG_OK(dbg_out_ok(gout + g, 4 * r), 25, gout + g, r)) {
+        if (r > 0u) gout[g] = q0;
+        if (r > 1u) gout[g + 1u] = q1;
+        if (r > 2u) gout[g + 2u] = q2;
+      }
     }
     uint8_t *g8 = (uint8_t *)gout;
     const uint32_t hi = ab >> 3, lo = ow < owf ? (rs & 3u) : 0u;
     if (ow >= owf && (rs & 3u)) {
-      for (uint32_t x = rs & 3u; x < 4u; x++) g8[(owf - 1u) * 4u + x] = (uint8_t)(first >> (8u * x));
+      for (uint32_t x = rs & 3u; x < 4u; x++)
+        if (DBG_OK(dbg_out_ok(g8 + (owf - 1u) * 4u + x, 1), 26, g8 + (owf - 1u) * 4u + x, rs))
+          g8[(owf - 1u) * 4u + x] = (uint8_t)(first >> (8u * x));
     }
-    for (uint32_t x = lo; x < hi; x++) g8[ow * 4u + x] = (uint8_t)(acc >> (8u * x));
+    for (uint32_t x = lo; x < hi; x++)
+      if (DBG_OK(dbg_out_ok(g8 + ow * 4u + x, 1), 27, g8 + ow * 4u + x, ow)) g8[ow * 4u + x] = (uint8_t)(acc >> (8u * x));
   }
   __device__ __forceinline__ uint32_t optr() const { return ow * 4u + (ab >> 3); }
 };
@@ -1106,7 +1147,7 @@ __device__ void decode_tile_long(const Smem &sm, WaveSmem &ws, const uint8_t *__
       const uint32_t o = 8u * k + (lane >> 3), c = (lane & 7u) ^ (lane >> 3);
       const uint64_t so = (uint64_t)__shfl((unsigned long long)src, (int)o);
       const uint32_t no = (uint32_t)__shfl((int)nck, (int)o);
-      if (c < no)  // chunks past the literal's last one stay unloaded: their bits are never consumed
+      if (c < no && DBG_OK(dbg_in_ok((const void *)(uintptr_t)(so + 16u * c), 16), 29, so + 16u * c, no))  // chunks past the literal's last one stay unloaded: their bits are never consumed
         __builtin_amdgcn_global_load_lds((g_void *)(uintptr_t)(so + 16u * c), (lds_void *)(ws.in_w + 256u * k), 16, 0,
                                          0);
     }
@@ -1343,6 +1384,8 @@ __device__ __forceinline__ void decode_body(Smem &sm, const uint8_t *__restrict_
     TL(tl_slot(tl_j, 1));
     // the previous tile's output and lengths leave, then this tile decodes
     if (pd_o) {
+      if (DBG_OK(dbg_out_ok(pd_o + pd_lo, pd_hi - pd_lo), 31, pd_o, pd_hi))
+        if (DBG_OK(dbg_out_ok(pd_o + pd_lo, pd_hi - pd_lo), 31, pd_o, pd_hi))
       store_out(pd_o, (const uint8_t *)ws.out_w, pd_lo, pd_hi, lane);
       flush_lens(ws, pd_s, pd_m, out_len, status, lane, kGaps ? str.kind : nullptr);
     }
@@ -1380,7 +1423,8 @@ __device__ __forceinline__ void decode_body(Smem &sm, const uint8_t *__restrict_
     tile3 = __builtin_amdgcn_readfirstlane(tile4);
   }
   if (pd_o) {
-    store_out(pd_o, (const uint8_t *)ws.out_w, pd_lo, pd_hi, lane);
+    if (DBG_OK(dbg_out_ok(pd_o + pd_lo, pd_hi - pd_lo), 31, pd_o, pd_hi))
+      store_out(pd_o, (const uint8_t *)ws.out_w, pd_lo, pd_hi, lane);
     flush_lens(ws, pd_s, pd_m, out_len, status, lane, kGaps ? str.kind : nullptr);
   }
   if (kGaps && str.kind) {
@@ -1403,7 +1447,8 @@ __device__ __forceinline__ void decode_body(Smem &sm, const uint8_t *__restrict_
             status[i] = (uint8_t)kStrEof;  // the block ended before the payload: io.EOF
           } else if (take) {
             DBG_CHECK(o0 + take <= out_off[i + 1], 13, o0, take);
-            copy_bytes(out + (o0 - out_bias), str.blk + st0, take);
+            if (DBG_OK(dbg_out_ok(out + (o0 - out_bias), take) && dbg_in_ok(str.blk + st0, take), 30, o0, take))
+              copy_bytes(out + (o0 - out_bias), str.blk + st0, take);
             out_len[i] = (uint32_t)take;
           }
         }

@@ -219,6 +219,8 @@ __global__ __launch_bounds__(kT) void read_fused_kernel(RsArgs a, const uint32_t
     // the previous tile's output and lengths leave (its kinds are read here,
     // before this tile's parse replaces them)
     if (pd_o) {
+      if (DBG_OK(dbg_out_ok(pd_o + pd_lo, pd_hi - pd_lo), 34, pd_o, pd_hi))
+        if (DBG_OK(dbg_out_ok(pd_o + pd_lo, pd_hi - pd_lo), 34, pd_o, pd_hi))
       store_out(pd_o, (const uint8_t *)ws.out_w, pd_lo, pd_hi, lane);
       flush_str(ws, pd_s, pd_m, kinds, a.out_len, a.status, lane);
     }
@@ -324,7 +326,8 @@ __global__ __launch_bounds__(kT) void read_fused_kernel(RsArgs a, const uint32_t
         const uint64_t st0 = a.sc_start[i], take = a.next[i] - st0;
         if (take) {
           DBG_CHECK(a.out_off[i] + take <= region_at(blk_len) && st0 + take <= blk_len, 12, a.out_off[i], take);
-          copy_bytes(a.out + a.out_off[i], a.blk + st0, take);
+          if (DBG_OK(dbg_out_ok(a.out + a.out_off[i], take) && dbg_in_ok(a.blk + st0, take), 33, a.out_off[i], take))
+            copy_bytes(a.out + a.out_off[i], a.blk + st0, take);
           a.out_len[i] = (uint32_t)take;
         } else if (kd & kDeclared) {
           a.status[i] = (uint8_t)kStrEof;  // the block ended before the payload: io.EOF
@@ -338,7 +341,8 @@ __global__ __launch_bounds__(kT) void read_fused_kernel(RsArgs a, const uint32_t
     tile3 = __builtin_amdgcn_readfirstlane(tile4);
   }
   if (pd_o) {
-    store_out(pd_o, (const uint8_t *)ws.out_w, pd_lo, pd_hi, lane);
+    if (DBG_OK(dbg_out_ok(pd_o + pd_lo, pd_hi - pd_lo), 34, pd_o, pd_hi))
+      store_out(pd_o, (const uint8_t *)ws.out_w, pd_lo, pd_hi, lane);
     flush_str(ws, pd_s, pd_m, kinds, a.out_len, a.status, lane);
   }
 }
@@ -501,6 +505,7 @@ hipError_t launch_read_fused(const DevTables &t, const uint8_t *blk, uint64_t bl
   const unsigned grid = (unsigned)((n + per_block - 1) / per_block);
   RsArgs a{blk, blk_len, pos, limit, prefix, n, out, out_off, next, out_len, status, sc_start, sc_hend, sc_kind,
            fallback, gen, wg_agg};
+  MHQ_DBG_SET_MEM(out, out + (blk_len / 5 * 8 + (blk_len % 5) * 8 / 5 + 1), blk, blk + ((blk_len + 15) & ~(uint64_t)15));
   read_fused_kernel<<<dim3(grid), dim3(kT), 0, s>>>(a, t.lut1, t.lut2, t.len, per_block, (uint32_t)tl);
   return hipGetLastError();
 }
@@ -523,6 +528,7 @@ hipError_t launch_read_fallback(const DevTables &t, const uint8_t *blk, uint64_t
   RsFallback f{RsArgs{blk, blk_len, pos, limit, prefix, n, out, out_off, next, out_len, status, sc_start, sc_hend,
                       sc_kind, fallback, gen, wg_agg},
                out_cap, wg_agg, wg_fin};
+  MHQ_DBG_SET_MEM(out, out + out_cap, blk, blk + ((blk_len + 15) & ~(uint64_t)15));
   read_fallback_kernel<<<dim3(grid), dim3(kT), 0, s>>>(f, t.lut1, t.lut2, t.len, per_block, (uint32_t)tl);
   return hipGetLastError();
 }
