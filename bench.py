@@ -132,17 +132,20 @@ def sum_over_ranks(pg, x: int) -> int:
 class Slot:
     """One rotating copy of every buffer of a round-trip step."""
 
-    def __init__(self, batch, enc_bytes, cap_bytes, dev):
+    def __init__(self, batch, enc_bytes, cap_bytes, dev, packed=False):
         import torch
 
         n = batch.n
         self.n = n
+        self.plain = batch.nbytes
         self.data = torch.from_numpy(batch.data).to(dev)
         self.off = torch.from_numpy(batch.off.view(np.int64)).to(dev)
         self.enc_len = torch.empty(n, dtype=torch.int32, device=dev)
         self.enc_off = torch.empty(n + 1, dtype=torch.int64, device=dev)
         self.cap_off = torch.empty(n + 1, dtype=torch.int64, device=dev)
-        self.enc = torch.empty(enc_bytes + 16, dtype=torch.uint8, device=dev)
+        # (the packed encode wants room for the most any plaintext encodes to)
+        self.enc = torch.empty(max(enc_bytes + 16, (30 * batch.nbytes + 7) // 8 if packed else 0), dtype=torch.uint8,
+                               device=dev)
         self.out = torch.empty(cap_bytes + 16, dtype=torch.uint8, device=dev)
         self.out_len = torch.empty(n, dtype=torch.int32, device=dev)
         self.status = torch.empty(n, dtype=torch.uint8, device=dev)
@@ -163,10 +166,17 @@ def encoded_sizes(codec, batch, dev):
     return int(s.enc_off[-1].item()), int(s.cap_off[-1].item())
 
 
+PACKED = True  # --encode packed: the encode side as one call (mhq_huff_encode_packed_dev)
+
+
 def round_trip(codec, s, stream=None):
-    # encode_len + offsets scan (one call, two launches), encode, decode
-    codec.encode_layout_dev(s.data, s.off, s.enc_len, s.enc_off, s.cap_off, stream=stream)
-    codec.encode_dev(s.data, s.off, s.enc, s.enc_off, stream=stream)
+    if PACKED:
+        # sizes, placement and codes in one launch (enc_packed.hip), decode
+        codec.encode_packed_dev(s.data, s.off, s.plain, s.enc_len, s.enc_off, s.cap_off, s.enc, stream=stream)
+    else:
+        # encode_len + offsets scan (one call, two launches), encode, decode
+        codec.encode_layout_dev(s.data, s.off, s.enc_len, s.enc_off, s.cap_off, stream=stream)
+        codec.encode_dev(s.data, s.off, s.enc, s.enc_off, stream=stream)
     codec.decode_dev(s.enc, s.enc_off, s.out, s.cap_off, s.out_len, s.status, stream=stream)
 
 
@@ -192,6 +202,10 @@ def kernel_ms(codec, slots, which, launches):
         s = slots[i % len(slots)]
         if which == "encode":
             codec.encode_dev(s.data, s.off, s.enc, s.enc_off)
+        elif which == "packed":
+            codec.encode_packed_dev(s.data, s.off, s.plain, s.enc_len, s.enc_off, s.cap_off, s.enc)
+        elif which == "layout":
+            codec.encode_layout_dev(s.data, s.off, s.enc_len, s.enc_off, s.cap_off)
         else:
             codec.decode_dev(s.enc, s.enc_off, s.out, s.cap_off, s.out_len, s.status)
 
@@ -676,6 +690,8 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-extras", action="store_true")
     ap.add_argument("--no-configs", action="store_true", help="skip the full-size configs 4 and 5")
+    ap.add_argument("--encode", choices=["packed", "split"], default="packed",
+                    help="the step's encode side: one call (packed) or the layout call + encode (split)")
     ap.add_argument("--streams", type=int, default=4, help="streams the batches alternate over (4: the hardware queues a process gets)")
     ap.add_argument("--traffic", default=os.path.join(REPO, "profiles", "pmc_traffic.json"))
     args = ap.parse_args()
@@ -698,10 +714,12 @@ def main():
 
     batch = workloads.make_batch(args.literals, "uniform", "hdr", workloads.SEED_NORTH_STAR + rank, 8, 64,
                                  f"config2: {args.literals} literals U{{8..64}} hdr")
+    global PACKED
+    PACKED = args.encode == "packed"
     enc_b, cap_b = encoded_sizes(codec, batch, dev)
-    first = Slot(batch, enc_b, cap_b, dev)
+    first = Slot(batch, enc_b, cap_b, dev, PACKED)
     R = max(2, int(np.ceil(args.rotate_gib * GIB / first.nbytes())))
-    slots = [first] + [Slot(batch, enc_b, cap_b, dev) for _ in range(R - 1)]
+    slots = [first] + [Slot(batch, enc_b, cap_b, dev, PACKED) for _ in range(R - 1)]
     for s in slots:  # correctness gate before timing
         round_trip(codec, s)
         verify_slot(s)
@@ -713,7 +731,7 @@ def main():
     S = max(1, args.streams)
     streams = [None] if S == 1 else [torch.cuda.Stream(device=dev).cuda_stream for _ in range(S)]
     if R % S:
-        slots += [Slot(batch, enc_b, cap_b, dev) for _ in range(S - R % S)]
+        slots += [Slot(batch, enc_b, cap_b, dev, PACKED) for _ in range(S - R % S)]
         R = len(slots)
         for s in slots:
             round_trip(codec, s)
@@ -747,6 +765,8 @@ def main():
     # per-kernel launch durations, live: the same slots, events only around
     # a run of back-to-back launches of one kernel on the launch stream
     enc_ms = kernel_ms(codec, slots, "encode", max(args.steps, 50))
+    lay_ms = kernel_ms(codec, slots, "layout", max(args.steps, 50))
+    pk_ms = kernel_ms(codec, slots, "packed", max(args.steps, 50)) if PACKED else None
     dec_ms = kernel_ms(codec, slots, "decode", max(args.steps, 50))
 
     plain_total = batch.nbytes * world * args.steps
@@ -770,13 +790,16 @@ def main():
         "dtype": "u8",
         "data": "synthetic",
         "config": {"workload": batch.name, "literals_per_gpu": batch.n, "plain_bytes_per_gpu": batch.nbytes,
-                   "encoded_bytes_per_gpu": enc_b, "step": "encode_len+offsets+encode+decode",
+                   "encoded_bytes_per_gpu": enc_b,
+                   "step": "encode_packed+decode" if PACKED else "encode_len+offsets+encode+decode",
                    "rotating_copies": R, "streams": S, "parallelism": f"shard{world} (independent literals, no collective)"},
         "roofline": {"bound": "hbm", "kernel": "decode", "achieved": round(achieved, 2),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": traffic, "traffic_source": os.path.relpath(args.traffic, REPO),
                      "alg_bytes_per_launch": alg, "ms_per_launch": round(dec_ms, 5)},
         "encode_ms_per_launch": round(enc_ms, 5),
+        "layout_ms_per_call": round(lay_ms, 5),
+        "packed_encode_ms_per_call": round(pk_ms, 5) if pk_ms is not None else None,
         "encode_hbm_frac": round(encode_algorithmic_bytes(batch.n, enc_b, batch.nbytes) / (enc_ms / 1e3) / 1e9
                                  / HBM_PEAK_GBS, 4),
     }
