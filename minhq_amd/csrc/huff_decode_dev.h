@@ -26,6 +26,14 @@
 #ifndef MHQ_DEC_BW  // 1: the fast loop stores each step's output bytes straight (unaligned ds_write_b32), see win_step_w
 #define MHQ_DEC_BW 0
 #endif
+// The decode's out-of-line helpers (the checked loop, the streamed long
+// literals, the head repair): called functions, or inlined where they are
+// used (-DMHQ_DEC_INLINE_CALLS=1, an experiment)
+#if defined(MHQ_DEC_INLINE_CALLS) && MHQ_DEC_INLINE_CALLS
+#define MHQ_CALLEE __forceinline__
+#else
+#define MHQ_CALLEE __noinline__
+#endif
 #ifndef MHQ_DEC_WOUT  // a wave's output slice (bytes, multiple of 16)
 #define MHQ_DEC_WOUT 6448
 #endif
@@ -375,7 +383,7 @@ __device__ __forceinline__ bool win_step_w(const Smem &sm, WinBuf3 &in, uint32_t
 // [p, endbit), output at slice byte optr), stored again byte by byte: the
 // bytes a neighbour's end stores (win_step_w) clobbered.  The literal is
 // known to decode to at least cnt bytes.
-[[maybe_unused]] __device__ __noinline__ void repair_head(const Smem &sm, WaveSmem &ws, uint32_t p, uint32_t optr, uint32_t cnt) {
+[[maybe_unused]] __device__ MHQ_CALLEE void repair_head(const Smem &sm, WaveSmem &ws, uint32_t p, uint32_t optr, uint32_t cnt) {
   uint8_t *o = (uint8_t *)ws.out_w + optr;
   for (uint32_t k = 0; k < cnt;) {
     if (!DBG_OK(dbg_lds_ok(o + k, 2) && dbg_lds_ok(ws.in_w + (p >> 5), 8), 32, optr + k, p)) break;
@@ -435,7 +443,7 @@ struct BitBufS {
 // decodes literal bits [p, endbit) into staging bytes [optr, oend) one probe
 // at a time, with the reference's end-of-literal and buffer-full rules
 // (hc/huffman.go:102-121).  Returns out_len | status << 31.
-__device__ __noinline__ uint32_t decode_checked(const Smem &sm, WaveSmem &ws, uint32_t p, uint32_t endbit,
+__device__ MHQ_CALLEE uint32_t decode_checked(const Smem &sm, WaveSmem &ws, uint32_t p, uint32_t endbit,
                                                 uint32_t optr, uint32_t oend) {
   BitBuf in;
   in.init(ws.in_w, p);
@@ -1068,7 +1076,7 @@ __device__ __forceinline__ void long_step(const Smem &sm, uint32_t *otgt, BB &in
 }
 
 template <bool kGaps>
-__device__ void decode_tile_long(const Smem &sm, WaveSmem &ws, const uint8_t *__restrict__ in,
+__device__ MHQ_CALLEE void decode_tile_long(const Smem &sm, WaveSmem &ws, const uint8_t *__restrict__ in,
                                  const uint64_t *__restrict__ in_off, const uint32_t *__restrict__ in_end,
                                  uint64_t in_bias, uint8_t *__restrict__ out,
                                  const uint64_t *__restrict__ out_off, uint64_t out_bias,

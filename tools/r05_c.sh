@@ -11,6 +11,12 @@ rc=$?
 echo "repro rc=$rc"; tail -12 "$OUT/repro_bw_dbg_shuffled.txt"
 grep -q "illegal memory access" "$OUT/repro_bw_dbg_shuffled.txt" && exit 1
 [ $rc -eq 0 ] || exit 1
+timeout -k 10 300 env MHQ_LIB_PATH=build/v/lib_bw_dbg_inl.so python3 -u tools/dbg/read_fault_repro.py shuffled \
+  > "$OUT/repro_bw_dbg_inl_shuffled.txt" 2>&1
+rc=$?
+echo "repro (helpers inlined) rc=$rc"; tail -6 "$OUT/repro_bw_dbg_inl_shuffled.txt"
+grep -q "illegal memory access" "$OUT/repro_bw_dbg_inl_shuffled.txt" && exit 1
+[ $rc -eq 0 ] || exit 1
 T="python3 -u -m pytest -x -v --timeout 300 --timeout-method thread"
 timeout -k 10 600 $T tests/test_encode_packed.py > "$OUT/packed_tests.txt" 2>&1 || { echo "packed tests failed"; tail -30 "$OUT/packed_tests.txt"; exit 1; }
 tail -2 "$OUT/packed_tests.txt"
