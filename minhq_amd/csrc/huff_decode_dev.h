@@ -23,16 +23,15 @@
 #ifndef MHQ_DEC_STEPS_GAPS  // the same for the in_end decode of framed strings (read_strings)
 #define MHQ_DEC_STEPS_GAPS 2
 #endif
-#ifndef MHQ_DEC_BW  // 1: the fast loop stores each step's output bytes straight (unaligned ds_write_b32), see win_step_w
-#define MHQ_DEC_BW 0
-#endif
 // The decode's out-of-line helpers (the checked loop, the streamed long
 // literals, the head repair): called functions, or inlined where they are
 // used (-DMHQ_DEC_INLINE_CALLS=1, an experiment)
 #if defined(MHQ_DEC_INLINE_CALLS) && MHQ_DEC_INLINE_CALLS
 #define MHQ_CALLEE __forceinline__
+#define MHQ_CALLEE_LONG __forceinline__
 #else
 #define MHQ_CALLEE __noinline__
+#define MHQ_CALLEE_LONG  // (the compiler's choice: inlined into the plain decode, called by the read kernels)
 #endif
 #ifndef MHQ_DEC_WOUT  // a wave's output slice (bytes, multiple of 16)
 #define MHQ_DEC_WOUT 6448
@@ -342,67 +341,6 @@ __device__ __forceinline__ bool win_step32(const Smem &sm, WinBuf3 &in, OutAccL 
   return stop || in.left < 0;
 }
 
-// The step with its output stored straight: the step's <= 4 bytes (two LUT1
-// entries' symbol half-words, the second shifted past the first's bits) go
-// to the staging as ONE unaligned ds_write_b32 at the output position `pb`
-// (an LDS bit address: 8 * byte address; the bytes past the step's own are
-// whatever the word held -- the literal's next step overwrites them), and
-// the position moves on by the step's bytes.  No 64-bit accumulator, no
-// read-modify-write: 5 vector instructions for the output instead of 14.
-// A finished literal keeps storing a word of zeros at its end, so the 4
-// bytes after a literal's output are clobbered: decode_piece repairs the
-// heads of the literals that follow a region with fewer than 4 bytes of
-// slack (repair_head).
-typedef uint32_t __attribute__((aligned(1))) u32_unaligned;
-typedef __attribute__((address_space(3))) u32_unaligned lds_u32_ua;
-template <bool kLong = true>
-__device__ __forceinline__ bool win_step_w(const Smem &sm, WinBuf3 &in, uint32_t &pb, bool &stop) {
-  const uint32_t S = in.top();
-  stop = S >= 0xfffffffcu;
-  uint32_t e = sm.lut1[S >> (32 - kLut1Bits)];
-  bool lng = false;
-  if (kLong && ((e == 0u) & !stop)) {  // a code of 13..29 bits (one branch: no short circuit)
-    uint32_t sym = 0;
-    const uint32_t L = long_code(sm.lut2, S, sym);
-    e = L | (8u << 8) | (sym << 16);
-    lng = true;
-  }
-  uint32_t e2 = sm.lut1[(S << (e & 31u)) >> (32 - kLut1Bits)];
-  e2 = lng ? 0u : e2;
-  const uint32_t w = (e >> 16) | ((e2 >> 16) << ((e >> 8) & 0xffu));
-  *(lds_u32_ua *)(uintptr_t)(pb >> 3) = w;
-  pb += ((e >> 8) & 0xffu) + ((e2 >> 8) & 0xffu);
-  const uint32_t n = (e & 0xffu) + (e2 & 0xffu);
-  in.pm += n;
-  in.left -= (int32_t)n;
-  in.set_mask();
-  return stop || in.left < 0;
-}
-
-// The first `cnt` output bytes of a literal decoded in the fast loop (bits
-// [p, endbit), output at slice byte optr), stored again byte by byte: the
-// bytes a neighbour's end stores (win_step_w) clobbered.  The literal is
-// known to decode to at least cnt bytes.
-[[maybe_unused]] __device__ MHQ_CALLEE void repair_head(const Smem &sm, WaveSmem &ws, uint32_t p, uint32_t optr, uint32_t cnt) {
-  uint8_t *o = (uint8_t *)ws.out_w + optr;
-  for (uint32_t k = 0; k < cnt;) {
-    if (!DBG_OK(dbg_lds_ok(o + k, 2) && dbg_lds_ok(ws.in_w + (p >> 5), 8), 32, optr + k, p)) break;
-    const uint32_t w0 = ws.in_w[p >> 5], w1 = ws.in_w[(p >> 5) + 1u];
-    const uint32_t S = (p & 31u) ? (w0 << (p & 31u)) | (w1 >> (32u - (p & 31u))) : w0;
-    const uint32_t e = sm.lut1[S >> (32 - kLut1Bits)];
-    if (e == 0u) {
-      uint32_t sym = 0;
-      p += long_code(sm.lut2, S, sym);
-      o[k++] = (uint8_t)sym;
-    } else {
-      o[k++] = (uint8_t)(e >> 16);
-      if (k < cnt && ((e >> 8) & 0xffu) == 16u) o[k++] = (uint8_t)(e >> 24);
-      p += sm.clen[(e >> 16) & 0xffu] + (((e >> 8) & 0xffu) == 16u ? sm.clen[e >> 24] : 0u);
-    }
-  }
-}
-
-
 // BitBuf over a long-path window (LDS-DMA): words left in memory byte order
 // (each is byte-swapped as it is read), and the window's 16-B chunks stored
 // XOR-swizzled: chunk c of lane l's window sits in slot c ^ (l % 8), so word k
@@ -501,11 +439,7 @@ struct LitRef {
   // The most this literal can produce stays inside the output slice (its
   // last word included): run past a short region, it can only spoil bytes
   // that a redo of the piece re-zeroes, or the slice's unused tail.
-  // (MHQ_DEC_BW: the step's word store reaches 3 bytes past the output, a
-  // code across the end 2 more)
-  __device__ __forceinline__ bool in_slice() const {
-    return optr + (endbit - p) / 5u + (MHQ_DEC_BW ? 8u : 4u) <= (uint32_t)kWOut + 16u;
-  }
+  __device__ __forceinline__ bool in_slice() const { return optr + (endbit - p) / 5u + 4u <= (uint32_t)kWOut + 16u; }
 };
 
 #ifdef MHQ_DIAG_TIMELINE  // diagnostic build: per-wave timeline (s_memrealtime, 100 MHz)
@@ -788,32 +722,6 @@ __device__ __forceinline__ void decode_piece(const Smem &sm, WaveSmem &ws, uint3
   const bool roomA = hasA && (A.roomy() || A.in_slice());
   const bool roomB = hasB && (B.roomy() || B.in_slice());
   uint32_t rA = kRedo, rB = kRedo;
-#if MHQ_DEC_BW
-  {
-    WinBuf3 in;
-    in.init(ws.in_w, roomA ? A.p : B.p, roomA ? A.endbit : B.endbit);
-    const uint32_t obase = (uint32_t)(uintptr_t)ws.out_w;  // the slice's LDS byte address
-    uint32_t pb = 8u * (obase + (roomA ? A.optr : B.optr));
-    uint32_t ost = obase + (roomA ? ostartA : ostartB);
-    bool onB = !roomA, active = roomA || roomB;
-    while (active) {
-      bool stop;
-#pragma unroll
-      for (int k = 1; k < kSteps; k++) win_step_w<false>(sm, in, pb, stop);
-      if (win_step_w<true>(sm, in, pb, stop)) {
-        const uint32_t r = in.left < 0 ? kRedo : ((pb >> 3) - ost) | ((uint32_t)(in.left > kEosOnes) << 31);
-        rA = onB ? rA : r;
-        rB = onB ? r : rB;
-        active = !onB && roomB;
-        in.init(ws.in_w, B.p, B.endbit);
-        pb = 8u * (obase + B.optr);
-        ost = obase + ostartB;
-        onB = true;
-      }
-      DBG_CHECK((pb >> 3) - obase + 4u <= (uint32_t)kWOut + 16u, 1, (pb >> 3) - obase, kSteps);
-    }
-  }
-#else
   {
     WinBuf3 in;
     in.init(ws.in_w, roomA ? A.p : B.p, roomA ? A.endbit : B.endbit);
@@ -847,7 +755,6 @@ __device__ __forceinline__ void decode_piece(const Smem &sm, WaveSmem &ws, uint3
     }
     atomicOr(pend.p, pend.v);
   }
-#endif
   // a lane that ran a literal through the fast loop and got no result crossed its end
   const bool crossed = (roomA && rA == kRedo) || (roomB && rB == kRedo);
   {
@@ -874,44 +781,9 @@ __device__ __forceinline__ void decode_piece(const Smem &sm, WaveSmem &ws, uint3
     }
   }
   TL(tls < 0 ? -1 : tls + 1);
-#if MHQ_DEC_BW
-  // The fast loop's end stores clobber the 4 bytes after each literal's
-  // output (win_step_w).  A literal that takes the checked loop without a
-  // redo (its region can truncate and the fast loop could overrun the slice)
-  // gets its region's head zeroed again first (the checked loop ORs into
-  // zeros); after the results, the literals of the fast loop whose
-  // predecessor's output ends less than 4 bytes before them (no slack: exact
-  // regions, a short or empty predecessor) get their first bytes stored again.
-  const bool fastA = hasA && rA != kRedo, fastB = hasB && rB != kRedo;
-  const bool any_fast = __ballot(fastA || fastB) != 0;  // (uniform: no redo)
-  if (any_fast) {
-    uint8_t *o8 = (uint8_t *)ws.out_w;
-    if (hasA && !roomA)
-      for (uint32_t x = A.optr; x < min(A.optr + 4u, A.oend); x++) o8[x] = 0;
-    if (hasB && !roomB)
-      for (uint32_t x = B.optr; x < min(B.optr + 4u, B.oend); x++) o8[x] = 0;
-    wave_sync();
-  }
   if (hasA) ws.len[A.lit] = rA != kRedo ? rA : decode_checked(sm, ws, A.p, A.endbit, A.optr, A.oend);
   if (hasB) ws.len[B.lit] = rB != kRedo ? rB : decode_checked(sm, ws, B.p, B.endbit, B.optr, B.oend);
   wave_sync();
-  if (any_fast) {
-    auto head = [&](const LitRef<kGaps> &X) {
-      if (X.lit == 0u) return 0u;
-      const uint32_t prev_end = (ws.rec[X.lit - 1u] >> 16) + (ws.len[X.lit - 1u] & 0x7fffffffu);
-      const uint32_t d = ws.len[X.lit] & 0x7fffffffu;
-      return prev_end + 4u > X.optr ? min(d, prev_end + 4u - X.optr) : 0u;
-    };
-    const uint32_t hA = fastA ? head(A) : 0u, hB = fastB ? head(B) : 0u;
-    if (hA) repair_head(sm, ws, A.p, A.optr, hA);
-    if (hB) repair_head(sm, ws, B.p, B.optr, hB);
-    wave_sync();
-  }
-#else
-  if (hasA) ws.len[A.lit] = rA != kRedo ? rA : decode_checked(sm, ws, A.p, A.endbit, A.optr, A.oend);
-  if (hasB) ws.len[B.lit] = rB != kRedo ? rB : decode_checked(sm, ws, B.p, B.endbit, B.optr, B.oend);
-  wave_sync();
-#endif
 }
 
 // ---- oversized tiles: literals streamed through per-lane windows ----------
@@ -1076,7 +948,7 @@ __device__ __forceinline__ void long_step(const Smem &sm, uint32_t *otgt, BB &in
 }
 
 template <bool kGaps>
-__device__ MHQ_CALLEE void decode_tile_long(const Smem &sm, WaveSmem &ws, const uint8_t *__restrict__ in,
+__device__ MHQ_CALLEE_LONG void decode_tile_long(const Smem &sm, WaveSmem &ws, const uint8_t *__restrict__ in,
                                  const uint64_t *__restrict__ in_off, const uint32_t *__restrict__ in_end,
                                  uint64_t in_bias, uint8_t *__restrict__ out,
                                  const uint64_t *__restrict__ out_off, uint64_t out_bias,
