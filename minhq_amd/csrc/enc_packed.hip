@@ -44,8 +44,7 @@ struct alignas(16) PackSmem {
   uint16_t order[kT];               // literals by ascending plaintext length
   uint32_t hist[kBuckets];
   uint32_t wsum[2][kT / kWave];     // per-wave totals of enc_len and capacity
-  uint32_t lb_stop[2];              // look-back: nearest inclusive prefix in the window (enc, cap)
-  unsigned long long lb_sum[2];     // look-back: the window's sums (enc, cap)
+  uint64_t base[2];                 // the range's place: enc and capacity bytes before it
 };
 
 struct PackArgs {
@@ -67,50 +66,73 @@ __device__ __forceinline__ uint64_t pack_slot(uint32_t tag, uint32_t flag, uint3
   return (uint64_t)tag << 34 | (uint64_t)flag << 32 | v;
 }
 
-// Sum of v over the workgroup, added to *dst (LDS, zeroed before the call).
-__device__ __forceinline__ void wg_add(unsigned long long *dst, uint64_t v) {
+// Sum of v over the 64 lanes of a wave (every lane gets it).
+__device__ __forceinline__ uint64_t wave_sum64(uint64_t v) {
 #pragma unroll
   for (int d = 1; d < kWave; d <<= 1) v += __shfl_xor((unsigned long long)v, d);
-  if (threadIdx.x % kWave == 0 && v) atomicAdd(dst, (unsigned long long)v);
+  return v;
 }
 
-// Totals (enc, cap) of workgroups [0, b): windows of kT predecessors, each
-// read in one round trip (spinning on slots not yet published), summed down
-// to the nearest inclusive prefix of each quantity.
-__device__ void look_back(const PackArgs &a, PackSmem &sm, uint32_t b, uint64_t &se, uint64_t &sc) {
-  const uint32_t tid = threadIdx.x;
+// Totals (enc, cap) of workgroups [0, b), by ONE wave: lane l reads the
+// slots of workgroup b - 1 - l (spinning until they carry the call's tag),
+// a ballot finds the nearest inclusive prefix of each quantity, and the
+// aggregates before it are added up with it; with none in the window, the
+// window's 64 aggregates are added and the next window is read.  (One wave
+// per workgroup polls, 64 slots per round trip, no workgroup barrier.)
+__device__ void look_back(const PackArgs &a, uint32_t b, uint32_t lane, uint64_t &se, uint64_t &sc) {
   se = sc = 0;
-  bool de = false, dc = false;  // (uniform)
-  for (int64_t hi = (int64_t)b - 1; hi >= 0 && !(de && dc); hi -= kT) {
-    const int64_t g = hi - (int64_t)tid;
+  bool de = false, dc = false;  // (uniform over the wave)
+  for (int64_t hi = (int64_t)b - 1; hi >= 0 && !(de && dc); hi -= kWave) {
+    const int64_t g = hi - (int64_t)lane;
     uint64_t ve = 0, vc = 0;
     if (g >= 0) {
       for (;;) {
         ve = __hip_atomic_load((unsigned long long *)a.slots + 2 * g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         vc = __hip_atomic_load((unsigned long long *)a.slots + 2 * g + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if ((uint32_t)(ve >> 34) == a.tag && (uint32_t)(vc >> 34) == a.tag) break;
-        __builtin_amdgcn_s_sleep(1);
+        __builtin_amdgcn_s_sleep(2);
       }
     }
-    if (tid == 0) {
-      sm.lb_stop[0] = sm.lb_stop[1] = kT;
-      sm.lb_sum[0] = sm.lb_sum[1] = 0;
-    }
-    __syncthreads();
-    if (g >= 0 && ((ve >> 32) & 3u) == 2u) atomicMin(&sm.lb_stop[0], tid);
-    if (g >= 0 && ((vc >> 32) & 3u) == 2u) atomicMin(&sm.lb_stop[1], tid);
-    __syncthreads();
-    const uint32_t stop_e = sm.lb_stop[0], stop_c = sm.lb_stop[1];
+    const uint64_t me = __ballot(g >= 0 && ((ve >> 32) & 3u) == 2u), mc = __ballot(g >= 0 && ((vc >> 32) & 3u) == 2u);
+    const uint32_t stop_e = me ? (uint32_t)__builtin_ctzll(me) : (uint32_t)kWave;
+    const uint32_t stop_c = mc ? (uint32_t)__builtin_ctzll(mc) : (uint32_t)kWave;
     // the aggregates before the nearest inclusive prefix, and that prefix
-    wg_add(&sm.lb_sum[0], (!de && g >= 0 && tid <= stop_e) ? (uint32_t)ve : 0u);
-    wg_add(&sm.lb_sum[1], (!dc && g >= 0 && tid <= stop_c) ? (uint32_t)vc : 0u);
-    __syncthreads();
-    se += de ? 0u : sm.lb_sum[0];
-    sc += dc ? 0u : sm.lb_sum[1];
-    de = de || stop_e < (uint32_t)kT;
-    dc = dc || stop_c < (uint32_t)kT;
-    __syncthreads();  // the window's LDS words are read before the next window resets them
+    const uint64_t xe = wave_sum64((!de && g >= 0 && lane <= stop_e) ? (uint32_t)ve : 0u);
+    const uint64_t xc = wave_sum64((!dc && g >= 0 && lane <= stop_c) ? (uint32_t)vc : 0u);
+    se += xe;
+    sc += xc;
+    de = de || stop_e < (uint32_t)kWave;
+    dc = dc || stop_c < (uint32_t)kWave;
   }
+}
+
+// Global bytes [lo, hi) from o_al (16-B aligned) <- staging bytes
+// [lo - shift, hi - shift): whole 16-B chunks as aligned stores of dwords
+// realigned from the staging (v_alignbyte), the bytes of the partial end
+// chunks one per thread (neighbours untouched).  lo >= shift.
+__device__ __forceinline__ void store_out_shifted(uint8_t *o_al, const uint32_t *stage, uint32_t lo, uint32_t hi,
+                                                  uint32_t shift, uint32_t tid, uint32_t nthreads) {
+  if (hi <= lo) return;
+  const uint32_t f0 = (lo + 15u) >> 4, f1 = hi >> 4;  // whole chunks [f0, f1)
+  const uint32_t r = shift & 3u;
+  for (uint32_t c = f0 + tid; c < f1; c += nthreads) {
+    const uint32_t x = 16u * c - shift;  // the chunk's first staging byte
+    const uint32_t w = x >> 2;
+    uint32_t d[5];
+#pragma unroll
+    for (int k = 0; k < 5; k++) d[k] = stage[w + (uint32_t)k];
+    u32x4 v;
+    v.x = __builtin_amdgcn_alignbyte(d[1], d[0], (x & 3u));
+    v.y = __builtin_amdgcn_alignbyte(d[2], d[1], (x & 3u));
+    v.z = __builtin_amdgcn_alignbyte(d[3], d[2], (x & 3u));
+    v.w = __builtin_amdgcn_alignbyte(d[4], d[3], (x & 3u));
+    __builtin_nontemporal_store(v, (u32x4 *)(o_al + 16u * c));
+  }
+  (void)r;
+  const uint32_t head_end = min(hi, f0 << 4), tail_start = max(head_end, f1 << 4);
+  const uint32_t y = tid < 16u ? lo + tid : tail_start + tid - 16u;
+  if (tid < 32u && y < (tid < 16u ? head_end : hi))
+    o_al[y] = (uint8_t)(stage[(y - shift) >> 2] >> (8u * ((y - shift) & 3u)));
 }
 
 // Code bits of global bytes [src, src + nbytes) (a range too large to stage).
@@ -165,7 +187,11 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu((kT / 64 * M
   if (tid < cnt) {
     uint64_t bits;
     if (staged) {
+#ifdef MHQ_X_PK_NOSIZE  // timing build only (wrong output): sizes guessed, no sizing pass
+      bits = (sm.rec[lit + 1] - sm.rec[lit]) * 6u;
+#else
       bits = encode_one<false>(sm, sm.rec[lit], sm.rec[lit + 1], 0u);
+#endif
     } else {
       const uint64_t s0 = a.in_off[L0 + tid];
       bits = size_literal_global(a.in + (s0 - a.in_bias), e_t - s0, sm.code);
@@ -191,45 +217,67 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu((kT / 64 * M
     C += sm.wsum[1][w];
   }
   const uint32_t rel_e = be + ve - v, rel_c = bc + vc - c;
-  // publish the range's totals, add up the predecessors', publish the prefix
+  // publish the range's totals at once, so that the ranges after it can
+  // add them up while this one encodes
   if (tid == 0) {
     __hip_atomic_store((unsigned long long *)a.slots + 2 * b, pack_slot(a.tag, 1u, T), __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store((unsigned long long *)a.slots + 2 * b + 1, pack_slot(a.tag, 1u, C), __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_AGENT);
   }
-  uint64_t base_e, base_c;
-  look_back(a, sm, b, base_e, base_c);
-  if (tid == 0) {
-    __hip_atomic_store((unsigned long long *)a.slots + 2 * b, pack_slot(a.tag, 2u, (uint32_t)(base_e + T)),
-                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store((unsigned long long *)a.slots + 2 * b + 1, pack_slot(a.tag, 2u, (uint32_t)(base_c + C)),
-                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  // encode into the staging at the range-relative offsets (the range's
+  // place in the output is not known yet: the store below realigns)
+  const bool staged_out = staged && T <= (uint32_t)kOutCap;  // (uniform)
+  if (staged_out) {
+    if (tid < cnt) sm.rel[tid] = rel_e;  // (every thread read its enc_len into v above)
+    for (uint32_t q = tid; q < (T + 15u) >> 4; q += kT) *(u32x4 *)(sm.out_w + 4u * q) = u32x4{0u, 0u, 0u, 0u};
+    __syncthreads();  // zeroed; sm.rel holds the offsets
+#ifndef MHQ_X_PK_NOENC  // (timing build only, wrong output: the layout alone)
+    if (tid < cnt) {
+      const uint32_t r = sm.rel[lit], len = (lit + 1u < cnt ? sm.rel[lit + 1] : T) - r;
+      if (len) encode_one<true>(sm, sm.rec[lit], sm.rec[lit + 1], r);
+    }
+#endif
   }
+  // the predecessors' totals (one wave), then this range's inclusive prefix
+  if (wave == 0) {
+    uint64_t se, sc;
+#ifdef MHQ_X_PK_NOLB  // timing build only (wrong output): no look-back, every range at its own guessed base
+    se = sc = (uint64_t)b * kT * 24u;
+#else
+    look_back(a, b, lane, se, sc);
+#endif
+    if (lane == 0) {
+      sm.base[0] = se;
+      sm.base[1] = sc;
+      __hip_atomic_store((unsigned long long *)a.slots + 2 * b, pack_slot(a.tag, 2u, (uint32_t)(se + T)),
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store((unsigned long long *)a.slots + 2 * b + 1, pack_slot(a.tag, 2u, (uint32_t)(sc + C)),
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  __syncthreads();  // the base; the staging complete
+  const uint64_t base_e = sm.base[0], base_c = sm.base[1];
   if (tid < cnt) {
     __builtin_nontemporal_store(v, a.enc_len + L0 + tid);
     a.out_off[L0 + tid] = a.base + base_e + rel_e;
     if (a.cap_off) a.cap_off[L0 + tid] = a.base + base_c + rel_c;
-    sm.rel[tid] = rel_e;
   }
   if (tid == 0 && L0 + cnt == n) {
     a.out_off[n] = a.base + base_e + T;
     if (a.cap_off) a.cap_off[n] = a.base + base_c + C;
   }
-  // encode: the literals whose regions end inside out_cap
-  const uint64_t fit_end = a.out_cap > base_e ? a.out_cap - base_e : 0u;  // range-relative bytes inside out
+#ifdef MHQ_X_PK_NOENC
+  return;
+#endif
+  // the codes: out + base_e on (never past out_cap, which the caller sized
+  // for the worst case: mhq_huff_encode_packed_dev)
+  const uint64_t room = a.out_cap > base_e ? a.out_cap - base_e : 0u;
   uint8_t *oa = a.out + base_e;
   const uint32_t odelta = (uint32_t)((uintptr_t)oa & 15u);
-  if (staged && T + odelta <= (uint32_t)kOutCap) {  // (uniform)
-    for (uint32_t q = tid; q < (T + odelta + 15u) >> 4; q += kT) *(u32x4 *)(sm.out_w + 4u * q) = u32x4{0u, 0u, 0u, 0u};
-    __syncthreads();  // zeroed; sm.rel holds the offsets
-    if (tid < cnt) {
-      const uint32_t r = sm.rel[lit], len = (lit + 1u < cnt ? sm.rel[lit + 1] : T) - r;
-      if (len && r + len <= fit_end) encode_one<true>(sm, sm.rec[lit], sm.rec[lit + 1], odelta + r);
-    }
-    __syncthreads();
-    store_out(oa - odelta, (const uint8_t *)sm.out_w, odelta, odelta + (uint32_t)min((uint64_t)T, fit_end), tid, kT);
-  } else if (tid < cnt && v && rel_e + v <= fit_end) {
+  if (staged_out) {
+    store_out_shifted(oa - odelta, sm.out_w, odelta, odelta + (uint32_t)min((uint64_t)T, room), odelta, tid, kT);
+  } else if (tid < cnt && v && rel_e + v <= room) {
     const uint64_t s0 = a.in_off[L0 + tid];
     encode_literal_global<true>(a.in + (s0 - a.in_bias), e_t - s0, oa + rel_e, sm.code, nullptr);
   }
