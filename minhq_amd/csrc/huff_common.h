@@ -14,6 +14,24 @@ namespace dev {
 constexpr int kWave = 64;
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
+#ifdef MHQ_DBG_CRUMBS
+// Diagnostic build (-DMHQ_DBG_CRUMBS): before each global access of the read
+// path a lane records (site, address) in pinned host memory, which the host
+// can still read after a GPU memory fault has taken the context down
+// (mhq_dbg_crumbs_dump, read_strings.hip).  Null: not recording.
+__device__ unsigned long long *g_crumbs;
+__device__ __forceinline__ void crumb(uint32_t site, const void *p) {
+  unsigned long long *c = g_crumbs;
+  if (!c) return;
+  c += 2ull * ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x);
+  __hip_atomic_store(c + 1, (unsigned long long)(uintptr_t)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store(c, (unsigned long long)site, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+#define CRUMB(site, p) ::mhq::dev::crumb((site), (const void *)(p))
+#else
+#define CRUMB(site, p) ((void)0)
+#endif
+
 // Orders this wave's LDS accesses (they retire in order per wave; this keeps
 // the compiler from moving them across a phase boundary).
 __device__ __forceinline__ void wave_sync() {
@@ -156,6 +174,7 @@ __device__ __forceinline__ void zero_lds(uint32_t *lds, uint32_t nbytes, int lan
 __device__ __forceinline__ void store_out(uint8_t *o_al, const uint8_t *lds, uint32_t lo, uint32_t hi, int lane,
                                           uint32_t nthreads = kWave) {
   if (hi <= lo) return;
+  CRUMB(40, o_al + hi - 1);
   const uint32_t f0 = (lo + 15u) >> 4, f1 = hi >> 4;  // whole chunks [f0, f1)
   for (uint32_t c = f0 + lane; c < f1; c += nthreads)
     __builtin_nontemporal_store(*(const u32x4 *)(lds + (c << 4)), (u32x4 *)(o_al + (c << 4)));
@@ -209,6 +228,8 @@ __device__ __forceinline__ void copy_bytes(uint8_t *__restrict__ dst, const uint
   const uint32_t h = (uint32_t)min((uint64_t)((0u - (uint32_t)(uintptr_t)dst) & 3u), len);
   const uint64_t body = (len - h) & ~(uint64_t)3;
   const uint32_t t = (uint32_t)(len - h) & 3u;
+  CRUMB(41, src + len - 1);
+  CRUMB(42, dst + len - 1);
   uint32_t hb[3], tb[3];
 #pragma unroll
   for (uint32_t k = 0; k < 3; k++) {

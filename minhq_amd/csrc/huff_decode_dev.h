@@ -20,8 +20,8 @@
 #ifndef MHQ_DEC_STEPS  // masked steps per end test of the probe loop (the plain decode)
 #define MHQ_DEC_STEPS 3
 #endif
-#ifndef MHQ_DEC_STEPS_GAPS  // the same for the in_end decode of framed strings (read_strings)
-#define MHQ_DEC_STEPS_GAPS 2
+#ifndef MHQ_DEC_STEPS_GAPS  // the same for the in_end decode of framed strings (read_strings; 3 since r05j: -1..-4 %)
+#define MHQ_DEC_STEPS_GAPS 3
 #endif
 // The decode's out-of-line helpers (the checked loop, the streamed long
 // literals, the head repair): called functions, or inlined where they are
@@ -163,10 +163,12 @@ __device__ void decode_literal_global(const uint8_t *src, uint64_t nbytes, uint8
     const uint64_t k = p >> 5;
     const uint32_t s = (uint32_t)p & 31u;
     const uint32_t *r0 = wb + (k < lastw ? k : lastw), *r1 = wb + (k + 1 < lastw ? k + 1 : lastw);
+    CRUMB(50, r1);
     const uint32_t w0 = DBG_OK(dbg_in_ok(r0, 4), 20, r0, src) ? __builtin_bswap32(*r0) : 0u;
     const uint32_t w1 = DBG_OK(dbg_in_ok(r1, 4), 20, r1, src) ? __builtin_bswap32(*r1) : 0u;
     const uint32_t win = s ? (w0 << s) | (w1 >> (32u - s)) : w0;
     const uint32_t e = sm.lut1[win >> (32 - kLut1Bits)];
+    CRUMB(51, dst + n);
     if (e == 0) {  // a long code or the EOS prefix
       const uint32_t nw = ~win;
       const uint32_t c = nw ? (uint32_t)__builtin_clz(nw) : 32u;
@@ -582,6 +584,7 @@ __device__ __forceinline__ void load_in(TileIn &t, const uint8_t *__restrict__ i
   const u32x4 *src = (const u32x4 *)(a - delta);
   const uint64_t need = ((iend - ib) + delta + 15u) >> 4;
   const uint32_t chunks = (uint32_t)min(need, (uint64_t)(kWIn / 16));
+  CRUMB(52, src + min(lane + (uint32_t)kWave * (kPF - 1), chunks - 1u));
 #pragma unroll
   for (int k = 0; k < kPF; k++) {
     const uint32_t c = min(lane + (uint32_t)kWave * k, chunks - 1u);
@@ -841,6 +844,7 @@ struct OutAccG {
     const bool full = ab >= 32u;
     const uint32_t v = (uint32_t)acc;
     if (full && ow >= owf) {
+      CRUMB(53, gout + ow);
       if (!grouped(ow)) {
         if (DBG_OK(dbg_out_ok(gout + ow, 4), 23, gout + ow, ow)) gout[ow] = v;
       } else {
@@ -861,6 +865,7 @@ struct OutAccG {
   __device__ __forceinline__ void finish(uint32_t *gout) {
     flush(gout);
     // whole words of the last, incomplete 16-B group
+    CRUMB(54, gout + ow);
     if (grouped(ow)) {
       const uint32_t r = (ow + ga) & 3u, g = ow - r;
       if (DBG_OK(dbg_out_ok(gout + g, 4 * r), 25, gout + g, r)) {
@@ -971,6 +976,7 @@ __device__ MHQ_CALLEE_LONG void decode_tile_long(const Smem &sm, WaveSmem &ws, c
   auto next_lit = [&]() {
     have = false;
     while (j < cnt) {
+      CRUMB(55, in_off + s + j);
       ib = in_off[s + j];
       if (kGaps) {  // the end's low word: the end is the first at or after ib with it
         const uint32_t e = in_end[s + j];
@@ -979,9 +985,11 @@ __device__ MHQ_CALLEE_LONG void decode_tile_long(const Smem &sm, WaveSmem &ws, c
       } else {
         ie = in_off[s + j + 1];
       }
+      CRUMB(56, out_off + s + j + 1);
       ob = out_off[s + j];
       const uint64_t oe = out_off[s + j + 1];
       uint8_t *o = out + (ob - out_bias);
+      CRUMB(57, out_len + s + j);
       if (ie == ib) {  // nothing to read: Read at EOF
         uint32_t len = 0, st = 0;
         if (kGaps && str_kind) str_outcome(str_kind, s + j, len, st);
@@ -1027,6 +1035,7 @@ __device__ MHQ_CALLEE_LONG void decode_tile_long(const Smem &sm, WaveSmem &ws, c
       const uint32_t o = 8u * k + (lane >> 3), c = (lane & 7u) ^ (lane >> 3);
       const uint64_t so = (uint64_t)__shfl((unsigned long long)src, (int)o);
       const uint32_t no = (uint32_t)__shfl((int)nck, (int)o);
+      if (c < no) CRUMB(58, so + 16u * c);
       if (c < no && DBG_OK(dbg_in_ok((const void *)(uintptr_t)(so + 16u * c), 16), 29, so + 16u * c, no))  // chunks past the literal's last one stay unloaded: their bits are never consumed
         __builtin_amdgcn_global_load_lds((g_void *)(uintptr_t)(so + 16u * c), (lds_void *)(ws.in_w + 256u * k), 16, 0,
                                          0);
@@ -1055,6 +1064,7 @@ __device__ MHQ_CALLEE_LONG void decode_tile_long(const Smem &sm, WaveSmem &ws, c
         uint32_t got = acc.optr() - ostart, st2 = st;
         DBG_CHECK(got <= oreg, 6, got, oreg);
         acc.finish(gout);
+        CRUMB(59, out_len + s + j);
         if (kGaps && str_kind) str_outcome(str_kind, s + j, got, st2);
         out_len[s + j] = got;
         status[s + j] = (uint8_t)st2;

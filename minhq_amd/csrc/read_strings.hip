@@ -6,6 +6,12 @@
 
 #include "huff_decode_dev.h"
 
+#ifdef MHQ_DBG_CRUMBS
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#endif
+
 namespace mhq {
 namespace {
 
@@ -51,6 +57,9 @@ __device__ __forceinline__ void rs_load(RsTile &t, const RsArgs &a, uint64_t s, 
                                         uint32_t lane) {
   const uint32_t z = vzero();
   const uint64_t j0 = min(s + 2u * lane, L1 - 1u) + z, j1 = min(s + 2u * lane + 1u, L1 - 1u) + z;
+  CRUMB(1, a.limit + j1);
+  CRUMB(2, a.prefix + j1);
+  CRUMB(3, a.pos + min(min(s + (uint64_t)tl, L1), a.n - 1u));
   t.p0 = a.pos[j0];
   t.p1 = a.pos[j1];
   t.l0 = a.limit[j0];
@@ -124,6 +133,7 @@ __device__ __forceinline__ void flush_str(const WaveSmem &ws, uint64_t s, uint32
         len = 0;
         st = 0;
       }
+      CRUMB(4, status + s + j);
       __builtin_nontemporal_store(len, out_len + s + j);
       __builtin_nontemporal_store((uint8_t)st, status + s + j);
     }
@@ -220,8 +230,7 @@ __global__ __launch_bounds__(kT) void read_fused_kernel(RsArgs a, const uint32_t
     // before this tile's parse replaces them)
     if (pd_o) {
       if (DBG_OK(dbg_out_ok(pd_o + pd_lo, pd_hi - pd_lo), 34, pd_o, pd_hi))
-        if (DBG_OK(dbg_out_ok(pd_o + pd_lo, pd_hi - pd_lo), 34, pd_o, pd_hi))
-      store_out(pd_o, (const uint8_t *)ws.out_w, pd_lo, pd_hi, lane);
+        store_out(pd_o, (const uint8_t *)ws.out_w, pd_lo, pd_hi, lane);
       flush_str(ws, pd_s, pd_m, kinds, a.out_len, a.status, lane);
     }
     pd_o = nullptr;
@@ -241,22 +250,28 @@ __global__ __launch_bounds__(kT) void read_fused_kernel(RsArgs a, const uint32_t
         const uint32_t pf = (rt.pf >> (8 * h)) & 0xffu;
         const uint64_t pn = j + 1u < cnt ? (h ? nx : rt.p1) : pe;  // the next string's pos (order test)
         RsStr r = rs_parse(p, lim, pf, blk_len, lo, hi, [&](uint64_t q) -> uint32_t {
+          if (!fits) CRUMB(5, a.blk + q);
           return fits ? slice_byte(ws, (uint32_t)(q - ps) + idelta) : (uint32_t)a.blk[q];
         });
         if (r.far)  // a header octet outside the staged span: from global memory (bad below unless it failed)
-          r = rs_parse(p, lim, pf, blk_len, 0, blk_len, [&](uint64_t q) -> uint32_t { return a.blk[q]; });
+          r = rs_parse(p, lim, pf, blk_len, 0, blk_len, [&](uint64_t q) -> uint32_t {
+            CRUMB(6, a.blk + q);
+            return a.blk[q];
+          });
         bad |= r.start + r.take > min(pn, blk_len);  // read_parse_kernel's order test
         const uint32_t k = r.kind & 3u;
         const uint64_t hend = k == 1u ? r.start + r.take : r.start;
         const uint64_t reg = region_at(r.start), i = s + j;
         kinds |= r.kind << (4 * h);
         if (k == 0u) (h ? raw1 : raw0) = (uint32_t)r.take;
+        CRUMB(7, a.next + i);
         a.out_off[i] = reg;  // (streaming stores: 1.6 us slower)
         a.next[i] = k == 2u ? p : r.start + r.take;
         if (fits) {
           ws.rec[j] = (uint32_t)(r.start - ps + idelta) | (uint32_t)(reg - rs0 + odelta) << 16;
           ws.len[j] = (uint32_t)(hend - ps + idelta);
         } else {
+          CRUMB(8, a.sc_kind + i);
           a.sc_start[i] = r.start;
           a.sc_hend[i] = (uint32_t)hend;
           a.sc_kind[i] = (uint8_t)r.kind;
@@ -310,8 +325,12 @@ __global__ __launch_bounds__(kT) void read_fused_kernel(RsArgs a, const uint32_t
       // string's frame, then the long-literal decode over sc_*
       if (lane == 0 && s + cnt < a.n) {
         const uint64_t i = s + cnt;
+        CRUMB(9, a.out_off + i);
         const RsStr r = rs_parse(a.pos[i], min(a.limit[i], blk_len), a.prefix[i], blk_len, 0, blk_len,
-                                 [&](uint64_t q) -> uint32_t { return a.blk[q]; });
+                                 [&](uint64_t q) -> uint32_t {
+                                   CRUMB(10, a.blk + q);
+                                   return a.blk[q];
+                                 });
         a.out_off[i] = region_at(r.start);
       }
       __threadfence_block();
@@ -321,6 +340,7 @@ __global__ __launch_bounds__(kT) void read_fused_kernel(RsArgs a, const uint32_t
       __threadfence_block();
       for (uint32_t j = lane; j < cnt; j += kWave) {  // the lane that wrote string j's length
         const uint64_t i = s + j;
+        CRUMB(11, a.next + i);
         const uint8_t kd = a.sc_kind[i];
         if ((kd & 3u) != 0u) continue;
         const uint64_t st0 = a.sc_start[i], take = a.next[i] - st0;
@@ -486,6 +506,34 @@ __global__ __launch_bounds__(kT) void read_fallback_kernel(RsFallback f, const u
 
 // The decode's grid and tile length (launch_decode), the tile length cut to
 // what fits the slices at the block's mean frame (decode_kernel's kGaps rule).
+#ifdef MHQ_DBG_CRUMBS
+// -DMHQ_DBG_CRUMBS: read_fused_kernel's lanes leave (site, address) crumbs in
+// pinned host memory (huff_common.h); the last launch's arguments are kept
+// for mhq_dbg_crumbs_dump.
+unsigned long long *g_crumb_host;
+uint64_t g_crumb_lanes, g_crumb_geom[3];
+RsArgs g_crumb_args;
+void crumbs_arm(const RsArgs &a, unsigned grid, uint64_t per_block, uint64_t tl, hipStream_t s) {
+  const uint64_t lanes = (uint64_t)std::max<unsigned>(grid, kReadFallbackMaxWgs) * kT;
+  (void)hipStreamSynchronize(s);
+  if (lanes > g_crumb_lanes) {
+    if (g_crumb_host) (void)hipHostFree(g_crumb_host);
+    g_crumb_host = nullptr;
+    if (hipHostMalloc((void **)&g_crumb_host, lanes * 16, hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess)
+      return;
+    g_crumb_lanes = lanes;
+  }
+  memset(g_crumb_host, 0, g_crumb_lanes * 16);
+  unsigned long long *d = nullptr;
+  (void)hipHostGetDevicePointer((void **)&d, g_crumb_host, 0);
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(g_crumbs), &d, sizeof(d));
+  g_crumb_args = a;
+  g_crumb_geom[0] = grid;
+  g_crumb_geom[1] = per_block;
+  g_crumb_geom[2] = tl;
+}
+#endif
+
 hipError_t launch_read_fused(const DevTables &t, const uint8_t *blk, uint64_t blk_len, const uint64_t *pos,
                              const uint64_t *limit, const uint8_t *prefix, uint64_t n, uint8_t *out,
                              uint64_t *out_off, uint32_t *out_len, uint8_t *status, uint64_t *next,
@@ -506,9 +554,13 @@ hipError_t launch_read_fused(const DevTables &t, const uint8_t *blk, uint64_t bl
   RsArgs a{blk, blk_len, pos, limit, prefix, n, out, out_off, next, out_len, status, sc_start, sc_hend, sc_kind,
            fallback, gen, wg_agg};
   MHQ_DBG_SET_MEM(out, out + (blk_len / 5 * 8 + (blk_len % 5) * 8 / 5 + 1), blk, blk + ((blk_len + 15) & ~(uint64_t)15));
+#ifdef MHQ_DBG_CRUMBS
+  crumbs_arm(a, grid, per_block, tl, s);
+#endif
   read_fused_kernel<<<dim3(grid), dim3(kT), 0, s>>>(a, t.lut1, t.lut2, t.len, per_block, (uint32_t)tl);
   return hipGetLastError();
 }
+
 
 // The fallback's grid and tile length are launch_decode's (its parse and
 // scan phases work on the decode's workgroup ranges).
@@ -535,6 +587,26 @@ hipError_t launch_read_fallback(const DevTables &t, const uint8_t *blk, uint64_t
 
 #ifdef MHQ_DBG_BOUNDS
 MHQ_DBG_READER(mhq_dbg_bounds_read)
+#endif
+
+#ifdef MHQ_DBG_CRUMBS
+extern "C" int mhq_dbg_crumbs_dump(const char *path) {
+  FILE *f = fopen(path, "wb");
+  if (!f) return -1;
+  const uint64_t hdr[24] = {0x6d6871637275ull, g_crumb_lanes, (uint64_t)g_crumb_args.blk, g_crumb_args.blk_len,
+                            (uint64_t)g_crumb_args.pos, (uint64_t)g_crumb_args.limit,
+                            (uint64_t)g_crumb_args.prefix, g_crumb_args.n, (uint64_t)g_crumb_args.out,
+                            (uint64_t)g_crumb_args.out_off, (uint64_t)g_crumb_args.next,
+                            (uint64_t)g_crumb_args.out_len, (uint64_t)g_crumb_args.status,
+                            (uint64_t)g_crumb_args.sc_start, (uint64_t)g_crumb_args.sc_hend,
+                            (uint64_t)g_crumb_args.sc_kind, (uint64_t)g_crumb_args.fallback,
+                            (uint64_t)g_crumb_args.wg_agg, g_crumb_args.gen, g_crumb_geom[0], g_crumb_geom[1],
+                            g_crumb_geom[2], 0, 0};
+  fwrite(hdr, sizeof(hdr), 1, f);
+  if (g_crumb_host) fwrite(g_crumb_host, 16, g_crumb_lanes, f);
+  fclose(f);
+  return 0;
+}
 #endif
 
 }  // namespace mhq

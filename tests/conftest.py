@@ -40,6 +40,13 @@ def _dbg_bounds_records():
     (huff_decode_dev.h: LDS records, the fast loop's output word, the decode
     and read path's global stores): none may have been recorded."""
     yield
+    crumbs = os.environ.get("MHQ_CRUMBS_OUT")
+    if crumbs:  # a -DMHQ_DBG_CRUMBS build: the read path's last global accesses (kept after a GPU fault)
+        from minhq_amd import _lib
+
+        fn = getattr(_lib.load(), "mhq_dbg_crumbs_dump", None)
+        if fn is not None:
+            fn(crumbs.encode())
     if os.environ.get("MHQ_DBG_BOUNDS_CHECK") != "1":
         return
     import ctypes
