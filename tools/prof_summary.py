@@ -24,7 +24,8 @@ KERNELS = {"decode_kernel": "decode_kernel", "encode_kernel<true>": "encode_kern
            "encode_kernel<false>": "encode_len_kernel", "encode_len_kernel": "encode_len_kernel",
            "encode_coop_kernel": "encode_coop_kernel",
            "scan_apply_kernel": "scan_apply_kernel",
-           "scan_reduce_kernel": "scan_reduce_kernel", "scan_kernel": "scan_kernel"}
+           "scan_reduce_kernel": "scan_reduce_kernel", "scan_kernel": "scan_kernel",
+           "encode_packed_kernel": "encode_packed_kernel"}
 
 
 def short(name):
