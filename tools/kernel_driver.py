@@ -136,6 +136,38 @@ def etimeline_report(fn):
         f"round0 {d(3, 4)[gen == g].mean():.2f}" for g in range(4) if (gen == g).any()), file=sys.stderr)
 
 
+def pktimeline_report(fn, nwg):
+    """Summarises the MHQ_DIAG_PKTL build's per-workgroup stamps of the packed
+    encode (last launch): [0] start, [1] staged, [2] sorted, [3] sized, [4]
+    scanned + published, [5] wave 0 encoded, [6] look-back done, [7] base
+    barrier, [8] end."""
+    import ctypes
+
+    W, S = 8192, 16
+    buf = (ctypes.c_ulonglong * (W * S))()
+    fn(buf, W * S)
+    a = np.frombuffer(buf, dtype=np.uint64).reshape(W, S).astype(np.int64)[:nwg]
+    a = a[(a[:, 0] > 0) & (a[:, 8] > 0)]
+    t0 = a[:, 0].min()
+    st = (a[:, 0] - t0) / 100.0
+    end = (a[:, 8] - t0) / 100.0
+    print(f"pktl: {a.shape[0]} workgroups; start p25 {np.percentile(st, 25):.2f} p50 {np.percentile(st, 50):.2f} "
+          f"p75 {np.percentile(st, 75):.2f} max {st.max():.2f}; end p50 {np.median(end):.2f} max {end.max():.2f} us",
+          file=sys.stderr)
+    d = lambda k0, k1: (a[:, k1] - a[:, k0]) / 100.0  # noqa: E731
+    names = ["stage", "sort", "size", "scan+pub", "encode(w0)", "lookback", "barrier", "store"]
+    print("  per workgroup (mean us): " + " ".join(f"{nm} {d(k, k + 1).mean():.2f}" for k, nm in enumerate(names)) +
+          f" life {d(0, 8).mean():.2f}", file=sys.stderr)
+    gen = np.digitize(st, np.percentile(st, [25, 50, 75]))
+    print("  by start quartile: " + " | ".join(
+        f"q{g}: start {st[gen == g].mean():.1f} life {d(0, 8)[gen == g].mean():.2f} lb {d(5, 6)[gen == g].mean():.2f}"
+        for g in range(4) if (gen == g).any()), file=sys.stderr)
+    # concurrency: resident workgroups over time
+    tt = np.linspace(0, end.max(), 12)
+    res = [int(((st <= x) & (end > x)).sum()) for x in tt]
+    print("  resident over time: " + " ".join(f"{x:.1f}:{r}" for x, r in zip(tt, res)), file=sys.stderr)
+
+
 def wg_report(fn):
     """Summarises the MHQ_DIAG_WG build's stamps (last launch): stager tile
     timeline and decoder wait/work split, in us from the workgroup's start."""
@@ -175,7 +207,7 @@ def wg_report(fn):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--kernel", default="decode", choices=["decode", "encode", "encode_len", "offsets", "layout"])
+    ap.add_argument("--kernel", default="decode", choices=["decode", "encode", "encode_len", "offsets", "layout", "packed"])
     ap.add_argument("--config", default="northstar")
     ap.add_argument("--n", type=int, default=0)
     ap.add_argument("--iters", type=int, default=50)
@@ -211,7 +243,8 @@ def main():
         cap_bytes = int(cap_off[-1].item())
 
     per = {"decode": enc_bytes + cap_bytes + 16 * n, "encode": b.nbytes + enc_bytes + 16 * n,
-           "encode_len": b.nbytes + 12 * n, "offsets": 20 * n, "layout": b.nbytes + 32 * n}[args.kernel]
+           "encode_len": b.nbytes + 12 * n, "offsets": 20 * n, "layout": b.nbytes + 32 * n,
+           "packed": b.nbytes + enc_bytes + 28 * n}[args.kernel]
     R = max(2, int(np.ceil(args.rotate_gib * (1 << 30) / per)))
     slots = []
     for _ in range(R):
@@ -221,9 +254,10 @@ def main():
             s["out"] = torch.empty(cap_bytes + 16, dtype=torch.uint8, device=dev)
             s["len"] = torch.empty(n, dtype=torch.int32, device=dev)
             s["st"] = torch.empty(n, dtype=torch.uint8, device=dev)
-        elif args.kernel in ("encode", "encode_len", "layout"):
+        elif args.kernel in ("encode", "encode_len", "layout", "packed"):
             s["in"], s["off"], s["eoff"] = data.clone(), off.clone(), enc_off.clone()
-            s["out"] = torch.empty(enc_bytes + 16, dtype=torch.uint8, device=dev)
+            s["out"] = torch.empty((30 * b.nbytes + 7) // 8 if args.kernel == "packed" else enc_bytes + 16,
+                                   dtype=torch.uint8, device=dev)
             s["len"] = torch.empty(n, dtype=torch.int32, device=dev)
             s["o1"] = torch.empty_like(enc_off)
             s["o2"] = torch.empty_like(cap_off)
@@ -242,6 +276,8 @@ def main():
             codec.encode_len_dev(s["in"], s["off"], s["len"])
         elif args.kernel == "layout":
             codec.encode_layout_dev(s["in"], s["off"], s["len"], s["o1"], s["o2"])
+        elif args.kernel == "packed":
+            codec.encode_packed_dev(s["in"], s["off"], b.nbytes, s["len"], s["o1"], s["o2"], s["out"])
         else:
             codec.offsets_dev(s["len"], s["o1"], s["o2"])
 
@@ -274,6 +310,9 @@ def main():
     etl = getattr(_lib.load(), "mhq_diag_etimeline", None)
     if etl:
         etimeline_report(etl)
+    pk = getattr(_lib.load(), "mhq_diag_pktimeline", None)
+    if pk and args.kernel == "packed":
+        pktimeline_report(pk, (n + 511) // 512)
     tl = getattr(_lib.load(), "mhq_diag_timeline", None)
     if tl:
         timeline_report(tl)
@@ -284,7 +323,8 @@ def main():
     alg = {"decode": enc_bytes + b.nbytes + 16 * (n + 1) + 5 * n,
            "encode": b.nbytes + enc_bytes + 16 * (n + 1) + 4 * n,  # + 4n (enc_len)
            "encode_len": b.nbytes + 8 * (n + 1) + 4 * n, "offsets": 4 * n + 16 * (n + 1),
-           "layout": b.nbytes + 8 * (n + 1) + 8 * n + 16 * (n + 1)}[args.kernel]
+           "layout": b.nbytes + 8 * (n + 1) + 8 * n + 16 * (n + 1),
+           "packed": b.nbytes + enc_bytes + 8 * (n + 1) + 4 * n + 16 * (n + 1)}[args.kernel]
     print(json.dumps({"kernel": args.kernel, "config": b.name, "n": n, "plain": b.nbytes, "enc": enc_bytes,
                       "us_per_launch": round(ms * 1e3, 2), "plain_gib_s": round(b.nbytes / ms / 1e6 / 1.073741824, 2),
                       "alg_bytes": alg, "hbm_frac": round(alg / (ms / 1e3) / 8e12, 4), "rotating": R}))
