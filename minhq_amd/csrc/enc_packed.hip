@@ -35,6 +35,23 @@ namespace {
 
 using namespace dev;
 
+#ifdef MHQ_DIAG_PKTL  // diagnostic build: per-workgroup phase stamps (s_memrealtime, 100 MHz)
+// by range: [0] start, [1] staged, [2] sorted, [3] sized, [4] scanned +
+// published, [5] wave 0's encode done, [6] look-back done, [7] base barrier
+// passed, [8] end
+constexpr int kPkSlots = 16;
+constexpr int kPkWgs = 8192;
+__device__ unsigned long long g_pktl[kPkWgs * kPkSlots];
+#define PKTL(r, slot, cond)                                                                        \
+  do {                                                                                             \
+    if ((cond) && (r) < (uint64_t)kPkWgs) g_pktl[(r) * kPkSlots + (slot)] = wall_clock64();         \
+  } while (0)
+#else
+#define PKTL(r, slot, cond) \
+  do {                      \
+  } while (0)
+#endif
+
 struct alignas(16) PackSmem {
   uint2 code[256];                  // (code right-justified, length)
   uint32_t in_w[kInCap / 4 + 4];    // plaintext, natural byte order
@@ -146,6 +163,7 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu((kT / 64 * M
     PackArgs a, const uint32_t *__restrict__ g_code, const uint8_t *__restrict__ g_len) {
   __shared__ PackSmem sm;
   const uint32_t tid = threadIdx.x, lane = tid % kWave, wave = tid / kWave, b = blockIdx.x;
+  PKTL(b, 0, tid == 0);
   const uint64_t n = a.n, L0 = (uint64_t)b * kT;  // (the grid is ceil(n / kT): L0 < n)
   const uint32_t cnt = (uint32_t)min((uint64_t)kT, n - L0);
   const uint64_t ib = uniform64(vload(a.in_off, L0)), ie = uniform64(vload(a.in_off, L0 + cnt));
@@ -165,6 +183,7 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu((kT / 64 * M
   }
   if (tid < kBuckets) sm.hist[tid] = 0;
   __syncthreads();
+  PKTL(b, 1, tid == 0);
   // sizing: staged, in length order (the 64 literals of a wave alike)
   uint32_t lit = tid;
   if (staged) {
@@ -184,14 +203,11 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu((kT / 64 * M
     __syncthreads();
     lit = tid < cnt ? sm.order[tid] : tid;
   }
+  PKTL(b, 2, tid == 0);
   if (tid < cnt) {
     uint64_t bits;
     if (staged) {
-#ifdef MHQ_X_PK_NOSIZE  // timing build only (wrong output): sizes guessed, no sizing pass
-      bits = (sm.rec[lit + 1] - sm.rec[lit]) * 6u;
-#else
       bits = encode_one<false>(sm, sm.rec[lit], sm.rec[lit + 1], 0u);
-#endif
     } else {
       const uint64_t s0 = a.in_off[L0 + tid];
       bits = size_literal_global(a.in + (s0 - a.in_bias), e_t - s0, sm.code);
@@ -199,6 +215,7 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu((kT / 64 * M
     sm.rel[lit] = (uint32_t)((bits + 7u) >> 3);
   }
   __syncthreads();
+  PKTL(b, 3, tid == 0);
   // the range's layout: exclusive scans of enc_len and capacity, in literal order
   const uint32_t v = tid < cnt ? sm.rel[tid] : 0u;
   const uint32_t c = (uint32_t)((uint64_t)v * 8u / 5u);
@@ -225,6 +242,7 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu((kT / 64 * M
     __hip_atomic_store((unsigned long long *)a.slots + 2 * b + 1, pack_slot(a.tag, 1u, C), __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_AGENT);
   }
+  PKTL(b, 4, tid == 0);
   // encode into the staging at the range-relative offsets (the range's
   // place in the output is not known yet: the store below realigns)
   const bool staged_out = staged && T <= (uint32_t)kOutCap;  // (uniform)
@@ -232,21 +250,17 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu((kT / 64 * M
     if (tid < cnt) sm.rel[tid] = rel_e;  // (every thread read its enc_len into v above)
     for (uint32_t q = tid; q < (T + 15u) >> 4; q += kT) *(u32x4 *)(sm.out_w + 4u * q) = u32x4{0u, 0u, 0u, 0u};
     __syncthreads();  // zeroed; sm.rel holds the offsets
-#ifndef MHQ_X_PK_NOENC  // (timing build only, wrong output: the layout alone)
     if (tid < cnt) {
       const uint32_t r = sm.rel[lit], len = (lit + 1u < cnt ? sm.rel[lit + 1] : T) - r;
       if (len) encode_one<true>(sm, sm.rec[lit], sm.rec[lit + 1], r);
     }
-#endif
   }
   // the predecessors' totals (one wave), then this range's inclusive prefix
   if (wave == 0) {
+    PKTL(b, 5, lane == 0);
     uint64_t se, sc;
-#ifdef MHQ_X_PK_NOLB  // timing build only (wrong output): no look-back, every range at its own guessed base
-    se = sc = (uint64_t)b * kT * 24u;
-#else
     look_back(a, b, lane, se, sc);
-#endif
+    PKTL(b, 6, lane == 0);
     if (lane == 0) {
       sm.base[0] = se;
       sm.base[1] = sc;
@@ -257,6 +271,7 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu((kT / 64 * M
     }
   }
   __syncthreads();  // the base; the staging complete
+  PKTL(b, 7, tid == 0);
   const uint64_t base_e = sm.base[0], base_c = sm.base[1];
   if (tid < cnt) {
     __builtin_nontemporal_store(v, a.enc_len + L0 + tid);
@@ -267,9 +282,6 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu((kT / 64 * M
     a.out_off[n] = a.base + base_e + T;
     if (a.cap_off) a.cap_off[n] = a.base + base_c + C;
   }
-#ifdef MHQ_X_PK_NOENC
-  return;
-#endif
   // the codes: out + base_e on (never past out_cap, which the caller sized
   // for the worst case: mhq_huff_encode_packed_dev)
   const uint64_t room = a.out_cap > base_e ? a.out_cap - base_e : 0u;
@@ -281,6 +293,7 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu((kT / 64 * M
     const uint64_t s0 = a.in_off[L0 + tid];
     encode_literal_global<true>(a.in + (s0 - a.in_bias), e_t - s0, oa + rel_e, sm.code, nullptr);
   }
+  PKTL(b, 8, tid == 0);
 }
 
 __global__ void set_base_kernel(uint64_t *out_off, uint64_t *cap_off, uint64_t base) {
@@ -289,6 +302,17 @@ __global__ void set_base_kernel(uint64_t *out_off, uint64_t *cap_off, uint64_t b
 }
 
 }  // namespace
+
+#ifdef MHQ_DIAG_PKTL
+extern "C" int mhq_diag_pktimeline(unsigned long long *out, int n) {
+  const int m = n < kPkWgs * kPkSlots ? n : kPkWgs * kPkSlots;
+  hipDeviceSynchronize();
+  const int rc = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_pktl), m * sizeof(unsigned long long)) == hipSuccess ? kPkSlots : -1;
+  static unsigned long long zeros[kPkWgs * kPkSlots];
+  hipMemcpyToSymbol(HIP_SYMBOL(g_pktl), zeros, sizeof(zeros));
+  return rc;
+}
+#endif
 
 size_t encode_packed_slot_bytes(uint64_t n) { return 16u * ((n + kT - 1) / kT); }
 

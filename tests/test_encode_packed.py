@@ -102,6 +102,24 @@ def test_packed_unstaged_ranges(codec, oracle_mod):
     _run(codec, oracle_mod, data, off)
 
 
+def test_packed_staged_long_codes(codec, oracle_mod):
+    """Short literals with a sprinkling of bytes whose codes exceed 24 bits
+    (control and high bytes: the packed LDS table holds only the length for
+    them, the code comes from the global table) in staged ranges."""
+    from minhq_amd import hc, workloads as w
+
+    rng = np.random.default_rng(45)
+    b = w.north_star(60000)
+    lits = hc.unpack(b.data, b.off)
+    for i in range(0, len(lits), 3):
+        x = bytearray(lits[i])
+        for _ in range(max(1, len(x) // 12)):
+            x[int(rng.integers(0, len(x)))] = int(rng.choice([0, 1, 9, 10, 13, 22, 127, 128, 200, 254, 255]))
+        lits[i] = bytes(x)
+    data, off = hc.pack(lits)
+    _run(codec, oracle_mod, data, off)
+
+
 def test_packed_long_literals_path(codec, oracle_mod):
     """Mean literal over 40 bytes: the layout call and the encode, same results."""
     from minhq_amd import workloads as w
