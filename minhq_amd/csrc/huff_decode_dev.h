@@ -20,6 +20,9 @@
 #ifndef MHQ_DEC_STEPS  // masked steps per end test of the probe loop (the plain decode)
 #define MHQ_DEC_STEPS 3
 #endif
+#ifndef MHQ_DEC_PAIR  // 1: a group's steps in pairs on one window read (win_pair)
+#define MHQ_DEC_PAIR 1
+#endif
 #ifndef MHQ_DEC_STEPS_GAPS  // the same for the in_end decode of framed strings (read_strings; 3 since r05j: -1..-4 %)
 #define MHQ_DEC_STEPS_GAPS 3
 #endif
@@ -313,9 +316,11 @@ struct WinBuf3 {
   }
 };
 
-template <bool kLong = true>
-__device__ __forceinline__ bool win_step32(const Smem &sm, WinBuf3 &in, OutAccL &out, PendL &pend, bool &stop) {
-  const uint32_t S = in.top();
+// One step on a window's 32 bits S (win_step32: S read from LDS at the step;
+// win_pair: from three words read for two steps).
+template <bool kLong>
+__device__ __forceinline__ bool win_step_s(const Smem &sm, WinBuf3 &in, uint32_t S, OutAccL &out, PendL &pend,
+                                           bool &stop) {
   stop = S >= 0xfffffffcu;
   uint32_t e = sm.lut1[S >> (32 - kLut1Bits)];
   atomicOr(pend.p, pend.v);
@@ -341,6 +346,27 @@ __device__ __forceinline__ bool win_step32(const Smem &sm, WinBuf3 &in, OutAccL 
   out.op += t >> 5;
   out.ab &= 31u;
   return stop || in.left < 0;
+}
+
+template <bool kLong = true>
+__device__ __forceinline__ bool win_step32(const Smem &sm, WinBuf3 &in, OutAccL &out, PendL &pend, bool &stop) {
+  return win_step_s<kLong>(sm, in, in.top(), out, pend, stop);
+}
+
+// Two steps from one window read: three words from the first step's bit
+// position cover the second step's too (a step without LUT2 moves at most
+// 24 bits), so the second step's window comes from registers (one LDS round
+// trip less on the step chain).  The words past a literal are the slice's
+// look-ahead slack.
+template <bool kLongB>
+__device__ __forceinline__ bool win_pair(const Smem &sm, WinBuf3 &in, OutAccL &out, PendL &pend, bool &stop) {
+  typedef __attribute__((address_space(3))) const uint32_t lds_u32;
+  lds_u32 *w = (lds_u32 *)(uintptr_t)((in.pm >> 3) & ~3u);
+  const uint32_t k0 = in.pm >> 5, w0 = w[0], w1 = w[1], w2 = w[2];
+  win_step_s<false>(sm, in, __builtin_amdgcn_alignbit(w0, w1, ~in.pm) | in.msk, out, pend, stop);
+  const bool hi = (in.pm >> 5) != k0;
+  return win_step_s<kLongB>(sm, in, __builtin_amdgcn_alignbit(hi ? w1 : w0, hi ? w2 : w1, ~in.pm) | in.msk, out, pend,
+                            stop);
 }
 
 // BitBuf over a long-path window (LDS-DMA): words left in memory byte order
@@ -655,6 +681,7 @@ __device__ __forceinline__ void decode_piece(const Smem &sm, WaveSmem &ws, uint3
   // masked steps per end test: 3 for the plain decode (north star -2.7 %,
   // config 4 -7 %, print +3 %: profiles/r04c_decode_steps_ab.txt)
   constexpr int kSteps = kGaps ? MHQ_DEC_STEPS_GAPS : MHQ_DEC_STEPS;
+  constexpr bool kPair = MHQ_DEC_PAIR;
   for (uint32_t c = lane; c < (out_bytes + 15u) >> 4; c += kWave) *(u32x4 *)(ws.out_w + 4u * c) = u32x4{0u, 0u, 0u, 0u};
   // counting sort by encoded length, longest first
   ws.hist[lane] = 0;
@@ -740,9 +767,23 @@ __device__ __forceinline__ void decode_piece(const Smem &sm, WaveSmem &ws, uint3
       // consumed at the EOS prefix; `left` stays negative), so the last
       // step's result covers them all; only that step resolves codes of 13+
       // bits through LUT2 (the others leave them, consuming nothing)
+      // (kPair: the steps go in pairs on one window read, an odd one last:
+      // north star -3.6 %, config 2 -4 %, config 3 -2 %, print -2 %,
+      // profiles/r05u_decode_pair_ab.txt)
+      bool fin;
+      if constexpr (kPair) {
 #pragma unroll
-      for (int k = 1; k < kSteps; k++) win_step32<false>(sm, in, out, pend, stop);
-      if (win_step32<true>(sm, in, out, pend, stop)) {
+        for (int k = 0; k + 2 < kSteps; k += 2) win_pair<false>(sm, in, out, pend, stop);
+        if constexpr (kSteps % 2 == 0)
+          fin = win_pair<true>(sm, in, out, pend, stop);
+        else
+          fin = win_step32<true>(sm, in, out, pend, stop);
+      } else {
+#pragma unroll
+        for (int k = 1; k < kSteps; k++) win_step32<false>(sm, in, out, pend, stop);
+        fin = win_step32<true>(sm, in, out, pend, stop);
+      }
+      if (fin) {
         // stop: the EOS prefix (INVALID when a 31st bit of the literal
         // follows); left < 0: a code crossed the end (the piece is redone)
         const uint32_t r = in.left < 0 ? kRedo : (out.optr(ws.out_w) - ost) | ((uint32_t)(in.left > kEosOnes) << 31);
