@@ -369,6 +369,7 @@ __device__ __forceinline__ bool win_pair(const Smem &sm, WinBuf3 &in, OutAccL &o
                             stop);
 }
 
+
 // BitBuf over a long-path window (LDS-DMA): words left in memory byte order
 // (each is byte-swapped as it is read), and the window's 16-B chunks stored
 // XOR-swizzled: chunk c of lane l's window sits in slot c ^ (l % 8), so word k
