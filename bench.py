@@ -531,9 +531,9 @@ def config5(codec, dev, launches, rotate_bytes):
     dv = Dev(codec, data, off, dev)
     slots = decode_slots(dv, 0, n, rotate_bytes, dev)
 
-    def run(i):
+    def run(i):  # (the batch's encoded size given: mhq_huff_decode_sized_dev picks the long-literal form)
         s = slots[i % len(slots)]
-        codec.decode_dev(s.enc, s.enc_off, s.out, s.cap_off, s.out_len, s.status)
+        codec.decode_dev(s.enc, s.enc_off, s.out, s.cap_off, s.out_len, s.status, in_bytes=dv.enc_bytes)
 
     run(0)
     check_decode(dv, 0, n, slots[0])

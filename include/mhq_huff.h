@@ -145,6 +145,16 @@ int mhq_huff_encode_dev(mhq_ctx *ctx, int dev, const uint8_t *in, const uint64_t
 int mhq_huff_decode_dev(mhq_ctx *ctx, int dev, const uint8_t *in, const uint64_t *in_off, uint64_t n,
                         uint8_t *out, const uint64_t *out_off, uint32_t *out_len, uint8_t *status,
                         void *stream);
+/* mhq_huff_decode_dev for a caller that knows the batch's encoded bytes
+ * in_bytes = in_off[n] - in_off[0] (0: unknown, the same as
+ * mhq_huff_decode_dev): a mean literal over 64 encoded bytes then takes the
+ * long-literal form of the kernel (every tile would stream through per-lane
+ * windows anyway; that form runs them at 16 waves per CU instead of 12).
+ * Same results either way; the host-memory mhq_huff_decode reads in_bytes
+ * from its offsets itself. */
+int mhq_huff_decode_sized_dev(mhq_ctx *ctx, int dev, const uint8_t *in, const uint64_t *in_off, uint64_t n,
+                              uint64_t in_bytes, uint8_t *out, const uint64_t *out_off, uint32_t *out_len,
+                              uint8_t *status, void *stream);
 
 /* ---------------- string literals: H bit + prefix integer + payload --------
  * Batch Reader.ReadString(prefix) and Writer.WriteStringRaw(s, prefix, choice)

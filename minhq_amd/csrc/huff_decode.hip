@@ -59,6 +59,65 @@ __global__ __launch_bounds__(kT) void decode_kernel(const uint8_t *__restrict__ 
                      g_len, per_block, tl0);
 }
 
+// ---- batches of long literals: the streamed form alone, 16 waves per CU ----
+// When the mean literal is too long for tiles of 64 to fit the staging
+// slices (config 5: 438 encoded bytes), every tile of decode_kernel streams
+// through decode_tile_long, which needs only its per-lane windows -- not the
+// slices, the records or the sort -- and its loop is latency-bound at the
+// decode kernel's 12 waves per CU.  This kernel runs the same per-lane
+// windows (128 B a lane) with the tables only: 16 waves per CU, tiles of 64
+// literals (one a lane) taken from an LDS counter.
+#ifndef MHQ_DEC_LW_WAVES  // waves per workgroup of the long-literal form
+#define MHQ_DEC_LW_WAVES 16
+#endif
+#ifndef MHQ_DEC_LW_WORDS  // a lane's window in words (32: 128 B, 16: 64 B)
+#define MHQ_DEC_LW_WORDS 32
+#endif
+#ifndef MHQ_DEC_LW_BLOCKS  // its workgroups per CU
+#define MHQ_DEC_LW_BLOCKS 1
+#endif
+constexpr int kLWaves = MHQ_DEC_LW_WAVES;
+constexpr uint32_t kLWords = MHQ_DEC_LW_WORDS;
+struct LongWin {
+  uint32_t in_w[kWave * kLWords];
+};
+struct SmemL {
+  uint32_t lut1[kLut1Size];
+  uint16_t lut2[kLut2Size];
+  uint8_t clen[256];
+  uint32_t next_tile;
+  LongWin w[kLWaves];
+};
+
+__global__ __launch_bounds__(kLWaves * kWave, MHQ_DEC_LW_BLOCKS) void decode_long_kernel(
+    const uint8_t *__restrict__ in, const uint64_t *__restrict__ in_off, uint64_t in_bias, uint64_t n,
+    uint8_t *__restrict__ out, const uint64_t *__restrict__ out_off, uint64_t out_bias, uint32_t *__restrict__ out_len,
+    uint8_t *__restrict__ status, const uint32_t *__restrict__ g_lut1, const uint16_t *__restrict__ g_lut2,
+    const uint8_t *__restrict__ g_len, uint64_t per_block) {
+  __shared__ SmemL sm;
+  const uint32_t tid = threadIdx.x, lane = tid % kWave, wave = tid / kWave;
+  const uint64_t L0 = (uint64_t)blockIdx.x * per_block;
+  if (L0 >= n) return;
+  const uint64_t L1 = min(L0 + per_block, n);
+  static_assert(kLut2Size / 8 <= kLWaves * kWave, "table copy shape");
+  for (uint32_t i = tid; i < (uint32_t)(kLut1Size / 4); i += kLWaves * kWave) ((u32x4 *)sm.lut1)[i] = ((const u32x4 *)g_lut1)[i];
+  if (tid < (uint32_t)(kLut2Size / 8)) ((u32x4 *)sm.lut2)[tid] = ((const u32x4 *)g_lut2)[tid];
+  if (tid < 64u) ((uint32_t *)sm.clen)[tid] = ((const uint32_t *)g_len)[tid];
+  if (tid == 0) sm.next_tile = kLWaves;
+  __syncthreads();
+  const uint32_t ntiles = (uint32_t)((L1 - L0 + kWave - 1) / kWave);
+  uint32_t tile = wave;
+  while (tile < ntiles) {
+    const uint64_t s = L0 + (uint64_t)tile * kWave;
+    const uint32_t cnt = (uint32_t)min((uint64_t)kWave, L1 - s);
+    decode_tile_long_body<false, SmemL, LongWin, kLWords>(sm, sm.w[wave], in, in_off, nullptr, in_bias, out, out_off,
+                                                     out_bias, out_len, status, s, cnt, lane);
+    uint32_t t = 0;
+    if (lane == 0) t = atomicAdd(&sm.next_tile, 1u);
+    tile = __builtin_amdgcn_readfirstlane(t);
+  }
+}
+
 }  // namespace
 
 #ifdef MHQ_DIAG_TIMELINE
@@ -71,8 +130,17 @@ extern "C" int mhq_diag_timeline(unsigned long long *out, int n) {
 hipError_t launch_decode(const DevTables &t, const uint8_t *in, const uint64_t *in_off, uint64_t in_bias,
                          uint64_t n, uint8_t *out, const uint64_t *out_off, uint64_t out_bias,
                          uint32_t *out_len, uint8_t *status, hipStream_t s, const uint32_t *in_end,
-                         const StrFinish *str) {
+                         const StrFinish *str, uint64_t in_bytes) {
   if (n == 0) return hipSuccess;
+  if (!in_end && in_bytes > (uint64_t)kLongMean * n) {  // every tile would stream: the long-literal form
+    const uint64_t cus = (uint64_t)dev::device_cus();
+    const uint64_t blocks = cus * MHQ_DEC_LW_BLOCKS;
+    const uint64_t per_block = (((n + blocks - 1) / blocks + kWave - 1) / kWave) * kWave;
+    const unsigned grid = (unsigned)((n + per_block - 1) / per_block);
+    decode_long_kernel<<<dim3(grid), dim3(kLWaves * kWave), 0, s>>>(in, in_off, in_bias, n, out, out_off, out_bias,
+                                                                     out_len, status, t.lut1, t.lut2, t.len, per_block);
+    return hipGetLastError();
+  }
   // One workgroup per CU, each a contiguous range of whole wave tiles.  The
   // tile length (<= kTile) is chosen so that every wave gets the same number
   // of tiles: no wave idles through a last, partial round.  (A shorter first

@@ -151,8 +151,9 @@ __device__ __forceinline__ uint32_t long_code(const uint16_t *lut2, uint32_t win
 
 // One literal, one lane, straight from global memory: literals too large for
 // the staging slices.  Same decision rules as the staged loop.
+template <class SM>
 __device__ void decode_literal_global(const uint8_t *src, uint64_t nbytes, uint8_t *dst, uint64_t cap,
-                                      const Smem &sm, uint32_t *out_len, uint8_t *status) {
+                                      const SM &sm, uint32_t *out_len, uint8_t *status) {
   const uint8_t *a8 = src - ((uintptr_t)src & 3u);
   const uintptr_t a0 = (uintptr_t)a8;
   const uint32_t *wb = (const uint32_t *)a8;
@@ -931,8 +932,8 @@ struct OutAccG {
 
 // The checked loop of decode_checked on a window, with the lane's running
 // accumulator (roomy literals only: no buffer-full rule).  Returns the status.
-template <class BB>
-__device__ __forceinline__ uint32_t end_checked_g(const Smem &sm, const uint32_t *win, uint32_t p, uint32_t endbit,
+template <class BB, class SM>
+__device__ __forceinline__ uint32_t end_checked_g(const SM &sm, const uint32_t *win, uint32_t p, uint32_t endbit,
                                                   OutAccG &out, uint32_t *gout, uint32_t swz) {
   BB in;
   in.init(win, p, swz);
@@ -965,8 +966,8 @@ __device__ __forceinline__ uint32_t end_checked_g(const Smem &sm, const uint32_t
 // probe is resolved at once through LUT2 — long literals are where long
 // codes pile up (config 5 has nothing else), and the fast step would spend a
 // second LUT1 probe finding it again.  Same end rules as decode_checked.
-template <class Acc, class BB, bool kFlush = true>
-__device__ __forceinline__ void long_step(const Smem &sm, uint32_t *otgt, BB &in, Acc &out, uint32_t endbit,
+template <class Acc, class BB, bool kFlush = true, class SM = Smem>
+__device__ __forceinline__ void long_step(const SM &sm, uint32_t *otgt, BB &in, Acc &out, uint32_t endbit,
                                           int &lim, uint32_t &bad) {
   // Branch free: LUT1 and LUT2 are read together (independent addresses, one
   // LDS round trip) and the entry is selected after.  kLongOnes or more
@@ -994,16 +995,24 @@ __device__ __forceinline__ void long_step(const Smem &sm, uint32_t *otgt, BB &in
   if (kFlush) out.flush(otgt);
 }
 
-template <bool kGaps>
-__device__ MHQ_CALLEE_LONG void decode_tile_long(const Smem &sm, WaveSmem &ws, const uint8_t *__restrict__ in,
+// (decode_tile_long_body: always inlined -- the long-literal kernel's
+// register budget applies to it; decode_tile_long: the decode kernels' call,
+// inlined or not at the compiler's choice)
+template <bool kGaps, class SM, class W, uint32_t kW = kLongWords>
+__device__ __forceinline__ void decode_tile_long_body(const SM &sm, W &ws, const uint8_t *__restrict__ in,
                                  const uint64_t *__restrict__ in_off, const uint32_t *__restrict__ in_end,
                                  uint64_t in_bias, uint8_t *__restrict__ out,
                                  const uint64_t *__restrict__ out_off, uint64_t out_bias,
                                  uint32_t *__restrict__ out_len, uint8_t *__restrict__ status, uint64_t s,
                                  uint32_t cnt, uint32_t lane, const uint8_t *__restrict__ str_kind = nullptr) {
-  uint32_t *win = ws.in_w + lane * kLongWords;  // spans the input and output slices
-  const uint32_t swz = (lane & 7u) << 2;         // BitBufS: the window's chunk swizzle
-  constexpr uint32_t kWinBits = kLongWords * 32u;
+  // (W: the wave's LDS, whose in_w starts the windows: in the decode kernel
+  // they span the wave's input and output slices)
+  // (kW: the window's words, 32 or 16; kCpw of its 16-B chunks)
+  constexpr uint32_t kCpw = kW / 4u;
+  static_assert(kW == 32u || kW == 16u, "window of 8 or 4 chunks");
+  uint32_t *win = ws.in_w + lane * kW;
+  const uint32_t swz = (lane % kCpw) << 2;  // BitBufS: the window's chunk swizzle
+  constexpr uint32_t kWinBits = kW * 32u;
   constexpr uint32_t kSafe = kWinBits - 96u;  // fast steps stay below: 24 bits + two words of look-ahead
   uint32_t j = lane;
   bool have = false;
@@ -1067,14 +1076,14 @@ __device__ MHQ_CALLEE_LONG void decode_tile_long(const Smem &sm, WaveSmem &ws, c
       src = (uint64_t)(uintptr_t)a16;
       const uint8_t *last = in + (ie - in_bias) - 1;  // the literal's last byte
       DBG_CHECK(a <= last, 8, rel, ie - ib);
-      nck = min((uint32_t)(((uintptr_t)last - (uintptr_t)a16) >> 4) + 1u, kLongWords / 4u);
+      nck = min((uint32_t)(((uintptr_t)last - (uintptr_t)a16) >> 4) + 1u, kCpw);
       p = delta * 8u + (uint32_t)(rel & 7u);
       endw = p + (uint32_t)((ie - ib) * 8u - rel);  // the literal's end in window bits (may lie beyond)
     }
 #pragma unroll
-    for (uint32_t k = 0; k < kWave / 8u; k++) {
-      // slot lane % 8 of owner o's window takes chunk (lane % 8) ^ (o % 8)
-      const uint32_t o = 8u * k + (lane >> 3), c = (lane & 7u) ^ (lane >> 3);
+    for (uint32_t k = 0; k < kCpw; k++) {
+      // slot lane % kCpw of owner o's window takes chunk (lane % kCpw) ^ (o % kCpw)
+      const uint32_t o = (kWave / kCpw) * k + lane / kCpw, c = (lane % kCpw) ^ (o % kCpw);
       const uint64_t so = (uint64_t)__shfl((unsigned long long)src, (int)o);
       const uint32_t no = (uint32_t)__shfl((int)nck, (int)o);
       if (c < no) CRUMB(58, so + 16u * c);
@@ -1118,6 +1127,17 @@ __device__ MHQ_CALLEE_LONG void decode_tile_long(const Smem &sm, WaveSmem &ws, c
     }
     wave_sync();  // every lane is done reading its window (look-ahead reads reach the neighbour's)
   }
+}
+template <bool kGaps, class SM, class W>
+__device__ MHQ_CALLEE_LONG void decode_tile_long(const SM &sm, W &ws, const uint8_t *__restrict__ in,
+                                                 const uint64_t *__restrict__ in_off,
+                                                 const uint32_t *__restrict__ in_end, uint64_t in_bias,
+                                                 uint8_t *__restrict__ out, const uint64_t *__restrict__ out_off,
+                                                 uint64_t out_bias, uint32_t *__restrict__ out_len,
+                                                 uint8_t *__restrict__ status, uint64_t s, uint32_t cnt, uint32_t lane,
+                                                 const uint8_t *__restrict__ str_kind = nullptr) {
+  decode_tile_long_body<kGaps>(sm, ws, in, in_off, in_end, in_bias, out, out_off, out_bias, out_len, status, s, cnt,
+                               lane, str_kind);
 }
 
 // Slow path: a tile whose bytes exceed the slices, in greedy pieces staged

@@ -70,7 +70,10 @@ struct StrFinish {
 hipError_t launch_decode(const DevTables &t, const uint8_t *in, const uint64_t *in_off,
                          uint64_t in_bias, uint64_t n, uint8_t *out, const uint64_t *out_off,
                          uint64_t out_bias, uint32_t *out_len, uint8_t *status, hipStream_t s,
-                         const uint32_t *in_end = nullptr, const StrFinish *str = nullptr);
+                         const uint32_t *in_end = nullptr, const StrFinish *str = nullptr, uint64_t in_bytes = 0);
+// in_bytes (the batch's encoded bytes, 0 if unknown): a mean literal over
+// kLongMean bytes takes the long-literal form (decode_long_kernel)
+constexpr uint64_t kLongMean = 64;
 // read_strings in one pass (str_frame.hip, MHQ_RS_FUSED): the frames parsed
 // from each staged tile, decoded in place, raw payloads copied, every output
 // written; strings out of block order (or a header past the next string's

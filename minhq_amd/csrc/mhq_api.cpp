@@ -352,7 +352,8 @@ int run_chunk(Device *d, Stage &S, const HostJob &j, uint64_t a, uint64_t b) {
     MHQ_TRY(mhq::launch_encode(d->tables, din, din_off, in_bias, m, dout, dout_off, out_bias, s));
   } else {
     MHQ_TRY(mhq::launch_decode(d->tables, din, din_off, in_bias, m, dout, dout_off, out_bias,
-                               (uint32_t *)S.lens.p, (uint8_t *)S.status.p, s));
+                               (uint32_t *)S.lens.p, (uint8_t *)S.status.p, s, nullptr, nullptr,
+                               j.in_off[b] - j.in_off[a]));
     MHQ_TRY(hipMemcpyAsync(j.lens + a, S.lens.p, m * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
     MHQ_TRY(hipMemcpyAsync(j.status + a, S.status.p, m, hipMemcpyDeviceToHost, s));
   }
@@ -424,7 +425,7 @@ bool run_zero_copy(Device *d, const HostJob &j, uint64_t a, uint64_t b, int &rc)
       uint8_t *dst = (uint8_t *)zero_copy_view(d->ordinal, j.status + a, m, 0);
       if (!dl || !dst) return false;
       rc = hip_rc(mhq::launch_decode(d->tables, din, din_off, j.in_off[0], m, dout, dout_off, j.out_off[0], dl, dst,
-                                     s));
+                                     s, nullptr, nullptr, j.in_off[a + m] - j.in_off[a]));
     }
   }
   const int r = hip_rc(hipStreamSynchronize(s));
@@ -691,14 +692,20 @@ int mhq_huff_encode_dev(mhq_ctx *ctx, int dev, const uint8_t *in, const uint64_t
   return hip_rc(mhq::launch_encode(d->tables, in, in_off, 0, n, out, out_off, 0, (hipStream_t)stream));
 }
 
-int mhq_huff_decode_dev(mhq_ctx *ctx, int dev, const uint8_t *in, const uint64_t *in_off, uint64_t n,
-                        uint8_t *out, const uint64_t *out_off, uint32_t *out_len, uint8_t *status,
-                        void *stream) {
+int mhq_huff_decode_sized_dev(mhq_ctx *ctx, int dev, const uint8_t *in, const uint64_t *in_off, uint64_t n,
+                              uint64_t in_bytes, uint8_t *out, const uint64_t *out_off, uint32_t *out_len,
+                              uint8_t *status, void *stream) {
   Device *d = device(ctx, dev);
   if (!d || (n && (!in_off || !out_off || !out_len || !status))) return MHQ_EINVAL;
   MHQ_TRY(hipSetDevice(d->ordinal));
   return hip_rc(mhq::launch_decode(d->tables, in, in_off, 0, n, out, out_off, 0, out_len, status,
-                                   (hipStream_t)stream));
+                                   (hipStream_t)stream, nullptr, nullptr, in_bytes));
+}
+
+int mhq_huff_decode_dev(mhq_ctx *ctx, int dev, const uint8_t *in, const uint64_t *in_off, uint64_t n,
+                        uint8_t *out, const uint64_t *out_off, uint32_t *out_len, uint8_t *status,
+                        void *stream) {
+  return mhq_huff_decode_sized_dev(ctx, dev, in, in_off, n, 0, out, out_off, out_len, status, stream);
 }
 
 int mhq_read_strings_dev(mhq_ctx *ctx, int dev, const uint8_t *blk, uint64_t blk_len, const uint64_t *pos,

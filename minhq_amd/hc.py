@@ -393,8 +393,17 @@ class Codec:
         check(self._L.mhq_huff_encode_dev(self._h, dev, data.data_ptr(), off.data_ptr(), n, out.data_ptr(),
                                           out_off.data_ptr(), self._stream(stream)), "encode_dev")
 
-    def decode_dev(self, enc, off, out, cap_off, out_len, status, dev: int = 0, stream=None) -> None:
+    def decode_dev(self, enc, off, out, cap_off, out_len, status, dev: int = 0, stream=None,
+                   in_bytes: int = 0) -> None:
+        """mhq_huff_decode_dev; with in_bytes (the batch's encoded bytes,
+        off[n] - off[0]) mhq_huff_decode_sized_dev, which picks the
+        long-literal form for a mean literal over 64 encoded bytes."""
         n = off.numel() - 1
+        if in_bytes:
+            check(self._L.mhq_huff_decode_sized_dev(self._h, dev, enc.data_ptr(), off.data_ptr(), n, in_bytes,
+                                                    out.data_ptr(), cap_off.data_ptr(), out_len.data_ptr(),
+                                                    status.data_ptr(), self._stream(stream)), "decode_sized_dev")
+            return
         check(self._L.mhq_huff_decode_dev(self._h, dev, enc.data_ptr(), off.data_ptr(), n, out.data_ptr(),
                                           cap_off.data_ptr(), out_len.data_ptr(), status.data_ptr(),
                                           self._stream(stream)), "decode_dev")

@@ -52,6 +52,7 @@ def main():
     ap.add_argument("--rotate-gib", type=float, default=1.0)
     ap.add_argument("--check", default="", help="libs whose decode output must equal base's")
     ap.add_argument("--exact", action="store_true")
+    ap.add_argument("--sized", action="store_true", help="decode through mhq_huff_decode_sized_dev (the batch's encoded bytes given)")
     ap.add_argument("--json", default="")
     args = ap.parse_args()
 
@@ -116,7 +117,11 @@ def main():
             slots.append(s)
 
         def run(L, h, s):
-            if args.kernel == "decode":
+            if args.kernel == "decode" and args.sized and hasattr(L, "mhq_huff_decode_sized_dev"):
+                rc = L.mhq_huff_decode_sized_dev(h, 0, s["in"].data_ptr(), s["off"].data_ptr(), n, enc_bytes,
+                                                 s["out"].data_ptr(), s["cap"].data_ptr(), s["len"].data_ptr(),
+                                                 s["st"].data_ptr(), stream)
+            elif args.kernel == "decode":
                 rc = L.mhq_huff_decode_dev(h, 0, s["in"].data_ptr(), s["off"].data_ptr(), n, s["out"].data_ptr(),
                                            s["cap"].data_ptr(), s["len"].data_ptr(), s["st"].data_ptr(), stream)
             elif args.kernel == "encode":
