@@ -34,8 +34,8 @@
 #ifndef MHQ_ENC_BLOCKS  // resident workgroups per CU
 #define MHQ_ENC_BLOCKS 3
 #endif
-#ifndef MHQ_ENC_SHORT_MEAN  // mean plaintext bytes up to which a workgroup takes one range of kT literals
-#define MHQ_ENC_SHORT_MEAN 40
+#ifndef MHQ_ENC_SHORT_MEAN  // mean plaintext bytes up to which the thread form encodes (96 since r05ai: 40-96 B -16..-38 %)
+#define MHQ_ENC_SHORT_MEAN 96
 #endif
 #ifndef MHQ_ENC_SHORT_GENS  // resident generations of the short form's grid before its workgroups loop over ranges
 #define MHQ_ENC_SHORT_GENS 4
@@ -57,15 +57,17 @@ constexpr int kBuckets = 64;
 constexpr uint32_t kShortMean = MHQ_ENC_SHORT_MEAN;
 constexpr uint32_t kTinyMean = MHQ_ENC_TINY_MEAN;
 // The thread-per-literal kernel's batches: a mean literal over kTinyMean and
-// up to kShortMean bytes (config 2 and the north star); the cooperative
-// kernel takes the rest (shorter: config 3's QIF literals, 26.6 us against
-// 38.3; longer: configs 4 and 5).
+// up to kShortMean bytes (config 2, the north star, config 4's Zipf text --
+// 169 against 189 us at 2^22 -- and text up to a 96-B mean: -16 to -38 %,
+// profiles/r05ai_encode_forms.txt); the cooperative kernel takes the rest
+// (shorter: config 3's QIF literals, 26.6 us against 38.3; longer: config
+// 5's long codes, 158 against 331 us).
 __device__ __forceinline__ bool thread_form(uint64_t bytes, uint64_t n) {
   return bytes > (uint64_t)kTinyMean * n && bytes <= (uint64_t)kShortMean * n;
 }
 
-#ifndef MHQ_ENC_PERSIST_MEAN  // the thread kernel's persistent ranges above this mean literal (bytes)
-#define MHQ_ENC_PERSIST_MEAN MHQ_ENC_SHORT_MEAN
+#ifndef MHQ_ENC_PERSIST_MEAN  // the thread kernel's persistent ranges above this mean literal (bytes; one range of kT literals per workgroup below)
+#define MHQ_ENC_PERSIST_MEAN 40
 #endif
 #ifndef MHQ_ENC_QUAD  // the thread kernel puts a staged word's four codes at once when they fit 32 bits
 #define MHQ_ENC_QUAD 1

@@ -658,7 +658,7 @@ int mhq_huff_encode_packed_dev(mhq_ctx *ctx, int dev, const uint8_t *in, const u
   if (in_bytes > (UINT64_MAX - 7) / 30 || out_cap < (30 * in_bytes + 7) / 8) return MHQ_EINVAL;
   MHQ_TRY(hipSetDevice(d->ordinal));
   hipStream_t s = (hipStream_t)stream;
-  // one launch for short literals (the thread form's band, mean <= 40 B, and
+  // one launch for short literals (a mean <= 40 B: a range of 512 stages in 24 KB; and
   // every look-back sum under 2^32); otherwise the layout call and the
   // encode, whose forms suit long literals
   if (in_bytes < ((uint64_t)1 << 29) && in_bytes <= 40 * n) {

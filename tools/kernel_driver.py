@@ -35,6 +35,9 @@ def batch_for(name: str, n: int):
         return w.config4(n or (1 << 22))
     if name == "config5":
         return w.config5(n or (1 << 20))
+    if ":" in name:  # kind:lo:hi, e.g. uniform:8:96 or zipf:4:256 (hdr bytes, 2^20 literals)
+        kind, lo, hi = name.split(":")
+        return w.make_batch(n or (1 << 20), kind, "hdr", 12345, int(lo), int(hi), name)
     raise SystemExit(f"unknown config {name}")
 
 
