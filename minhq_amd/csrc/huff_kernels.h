@@ -73,7 +73,10 @@ hipError_t launch_decode(const DevTables &t, const uint8_t *in, const uint64_t *
                          const uint32_t *in_end = nullptr, const StrFinish *str = nullptr, uint64_t in_bytes = 0);
 // in_bytes (the batch's encoded bytes, 0 if unknown): a mean literal over
 // kLongMean bytes takes the long-literal form (decode_long_kernel)
-constexpr uint64_t kLongMean = 64;
+#ifndef MHQ_DEC_LONG_MEAN
+#define MHQ_DEC_LONG_MEAN 64
+#endif
+constexpr uint64_t kLongMean = MHQ_DEC_LONG_MEAN;
 // read_strings in one pass (str_frame.hip, MHQ_RS_FUSED): the frames parsed
 // from each staged tile, decoded in place, raw payloads copied, every output
 // written; strings out of block order (or a header past the next string's
