@@ -650,6 +650,9 @@ int mhq_huff_encode_layout_dev(mhq_ctx *ctx, int dev, const uint8_t *in, const u
   return hip_rc(e != hipSuccess ? e : e2);
 }
 
+#ifndef MHQ_PK_MAX_MEAN  // the packed encode's largest mean literal (bytes)
+#define MHQ_PK_MAX_MEAN 40
+#endif
 int mhq_huff_encode_packed_dev(mhq_ctx *ctx, int dev, const uint8_t *in, const uint64_t *in_off, uint64_t n,
                                uint64_t in_bytes, uint64_t base, uint32_t *enc_len, uint64_t *out_off,
                                uint64_t *cap_off, uint8_t *out, uint64_t out_cap, void *stream) {
@@ -661,7 +664,7 @@ int mhq_huff_encode_packed_dev(mhq_ctx *ctx, int dev, const uint8_t *in, const u
   // one launch for short literals (a mean <= 40 B: a range of 512 stages in 24 KB; and
   // every look-back sum under 2^32); otherwise the layout call and the
   // encode, whose forms suit long literals
-  if (in_bytes < ((uint64_t)1 << 29) && in_bytes <= 40 * n) {
+  if (in_bytes < ((uint64_t)1 << 29) && in_bytes <= (uint64_t)MHQ_PK_MAX_MEAN * n) {
     ScratchLease slots(d, d->slots, s, mhq::encode_packed_slot_bytes(n));
     if (slots.p) {
       static std::atomic<uint64_t> g_gen{0};
