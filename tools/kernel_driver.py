@@ -315,7 +315,7 @@ def main():
         etimeline_report(etl)
     pk = getattr(_lib.load(), "mhq_diag_pktimeline", None)
     if pk and args.kernel == "packed":
-        pktimeline_report(pk, (n + 511) // 512)
+        pktimeline_report(pk, min(8192, (n + 255) // 256))
     tl = getattr(_lib.load(), "mhq_diag_timeline", None)
     if tl:
         timeline_report(tl)
