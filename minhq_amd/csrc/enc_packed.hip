@@ -13,8 +13,8 @@
 //     offsets;
 //   * the range's totals are published (agent-scope atomic stores, tagged
 //     with the call), and a decoupled look-back adds up the predecessors'
-//     totals -- each window of 512 predecessors is read in one round trip and
-//     stops at the nearest published inclusive prefix -- then the range
+//     totals -- kLbW windows of 64 predecessors are read per round trip, and
+//     it stops at the nearest published inclusive prefix -- then the range
 //     publishes its own inclusive prefix;
 //   * enc_len, out_off and cap_off are written, and the staged plaintext is
 //     encoded into the zeroed output staging at the range's real alignment
@@ -90,36 +90,59 @@ __device__ __forceinline__ uint64_t wave_sum64(uint64_t v) {
   return v;
 }
 
+#ifndef MHQ_PK_LBW  // look-back windows of 64 predecessors read per round trip
+#define MHQ_PK_LBW 4
+#endif
+constexpr int kLbW = MHQ_PK_LBW;
+
 // Totals (enc, cap) of workgroups [0, b), by ONE wave: lane l reads the
-// slots of workgroup b - 1 - l (spinning until they carry the call's tag),
-// a ballot finds the nearest inclusive prefix of each quantity, and the
-// aggregates before it are added up with it; with none in the window, the
-// window's 64 aggregates are added and the next window is read.  (One wave
-// per workgroup polls, 64 slots per round trip, no workgroup barrier.)
+// slots of workgroups b - 1 - l - 64 k (k < kLbW windows at once, spinning
+// until they carry the call's tag), a ballot per window finds the nearest
+// inclusive prefix of each quantity, and the aggregates before it are added
+// up with it; with none in the windows, their aggregates are added and the
+// next kLbW windows are read.  (One wave per workgroup polls, no workgroup
+// barrier; in a generation of ranges started together the nearest inclusive
+// prefix can lie several windows back.)
 __device__ void look_back(const PackArgs &a, uint32_t b, uint32_t lane, uint64_t &se, uint64_t &sc) {
   se = sc = 0;
   bool de = false, dc = false;  // (uniform over the wave)
-  for (int64_t hi = (int64_t)b - 1; hi >= 0 && !(de && dc); hi -= kWave) {
-    const int64_t g = hi - (int64_t)lane;
-    uint64_t ve = 0, vc = 0;
-    if (g >= 0) {
-      for (;;) {
-        ve = __hip_atomic_load((unsigned long long *)a.slots + 2 * g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        vc = __hip_atomic_load((unsigned long long *)a.slots + 2 * g + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if ((uint32_t)(ve >> 34) == a.tag && (uint32_t)(vc >> 34) == a.tag) break;
-        __builtin_amdgcn_s_sleep(2);
+  const unsigned long long *sl = (const unsigned long long *)a.slots;
+  for (int64_t hi = (int64_t)b - 1; hi >= 0 && !(de && dc); hi -= (int64_t)kWave * kLbW) {
+    uint64_t ve[kLbW], vc[kLbW];
+#pragma unroll
+    for (int k = 0; k < kLbW; k++) {
+      const int64_t g = hi - (int64_t)kWave * k - (int64_t)lane;
+      ve[k] = vc[k] = 0;
+      if (g >= 0) {
+        ve[k] = __hip_atomic_load(sl + 2 * g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        vc[k] = __hip_atomic_load(sl + 2 * g + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     }
-    const uint64_t me = __ballot(g >= 0 && ((ve >> 32) & 3u) == 2u), mc = __ballot(g >= 0 && ((vc >> 32) & 3u) == 2u);
-    const uint32_t stop_e = me ? (uint32_t)__builtin_ctzll(me) : (uint32_t)kWave;
-    const uint32_t stop_c = mc ? (uint32_t)__builtin_ctzll(mc) : (uint32_t)kWave;
-    // the aggregates before the nearest inclusive prefix, and that prefix
-    const uint64_t xe = wave_sum64((!de && g >= 0 && lane <= stop_e) ? (uint32_t)ve : 0u);
-    const uint64_t xc = wave_sum64((!dc && g >= 0 && lane <= stop_c) ? (uint32_t)vc : 0u);
-    se += xe;
-    sc += xc;
-    de = de || stop_e < (uint32_t)kWave;
-    dc = dc || stop_c < (uint32_t)kWave;
+#pragma unroll
+    for (int k = 0; k < kLbW; k++) {
+      const int64_t g = hi - (int64_t)kWave * k - (int64_t)lane;
+      while (g >= 0 && ((uint32_t)(ve[k] >> 34) != a.tag || (uint32_t)(vc[k] >> 34) != a.tag)) {
+        __builtin_amdgcn_s_sleep(2);
+        ve[k] = __hip_atomic_load(sl + 2 * g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        vc[k] = __hip_atomic_load(sl + 2 * g + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < kLbW; k++) {
+      if (de && dc) break;
+      const int64_t g = hi - (int64_t)kWave * k - (int64_t)lane;
+      const uint64_t me = __ballot(g >= 0 && ((ve[k] >> 32) & 3u) == 2u);
+      const uint64_t mc = __ballot(g >= 0 && ((vc[k] >> 32) & 3u) == 2u);
+      const uint32_t stop_e = me ? (uint32_t)__builtin_ctzll(me) : (uint32_t)kWave;
+      const uint32_t stop_c = mc ? (uint32_t)__builtin_ctzll(mc) : (uint32_t)kWave;
+      // the aggregates before the nearest inclusive prefix, and that prefix
+      const uint64_t xe = wave_sum64((!de && g >= 0 && lane <= stop_e) ? (uint32_t)ve[k] : 0u);
+      const uint64_t xc = wave_sum64((!dc && g >= 0 && lane <= stop_c) ? (uint32_t)vc[k] : 0u);
+      se += xe;
+      sc += xc;
+      de = de || stop_e < (uint32_t)kWave;
+      dc = dc || stop_c < (uint32_t)kWave;
+    }
   }
 }
 

@@ -1,0 +1,12 @@
+#!/bin/bash
+# Round 5 call aw: the packed encode look-back reading 1, 2, 4, 8 windows per round trip (MHQ_PK_LBW) A/B, timeline, tests.
+set -o pipefail
+OUT=${1:-gpurun_out/r05aw}
+mkdir -p "$OUT"
+timeout -k 10 600 python3 tools/abmulti.py --kernel packed --reps 3 --configs config2,northstar,config3 \
+  --libs w1=build/v/lib_w1.so,w2=build/v/lib_w2.so,w4=minhq_amd/libmhq_huff.so,w8=build/v/lib_w8.so > "$OUT/ab.txt" 2>&1 || { cat "$OUT/ab.txt"; exit 1; }
+grep -v amdgpu.ids "$OUT/ab.txt"
+MHQ_LIB_PATH=build/v/lib_pktl.so timeout -k 10 120 python3 tools/kernel_driver.py --kernel packed --config config2 --iters 20 > "$OUT/pktl.txt" 2>&1 || { cat "$OUT/pktl.txt"; exit 1; }
+grep -v amdgpu.ids "$OUT/pktl.txt"
+timeout -k 10 300 python3 -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_encode_packed.py > "$OUT/tests.txt" 2>&1 || { tail -30 "$OUT/tests.txt"; exit 1; }
+tail -3 "$OUT/tests.txt"
