@@ -52,17 +52,34 @@ __device__ unsigned long long g_pktl[kPkWgs * kPkSlots];
   } while (0)
 #endif
 
+#ifndef MHQ_PK_BLOCKS  // resident workgroups per CU (LDS-bound: PackSmem; 4 since r05ax: config 2 -10 %, north star -7 %)
+#define MHQ_PK_BLOCKS 4
+#endif
+#ifndef MHQ_PK_INCAP  // plaintext staging (bytes)
+#define MHQ_PK_INCAP (MHQ_PK_BLOCKS >= 4 ? 20224 : MHQ_ENC_INCAP)
+#endif
+#ifndef MHQ_PK_OUTCAP  // output staging (bytes)
+#define MHQ_PK_OUTCAP (MHQ_PK_BLOCKS >= 4 ? 15360 : MHQ_ENC_OUTCAP)
+#endif
+constexpr int kPkIn = MHQ_PK_INCAP, kPkOut = MHQ_PK_OUTCAP;
+
 struct alignas(16) PackSmem {
   uint2 code[256];                  // (code right-justified, length)
-  uint32_t in_w[kInCap / 4 + 4];    // plaintext, natural byte order
-  uint32_t out_w[kOutCap / 4 + 4];  // output staging (global alignment, zero-filled)
-  uint32_t rec[kT + 1];             // literal boundaries: input byte index from the 16-B aligned start
+  uint32_t in_w[kPkIn / 4 + 4];     // plaintext, natural byte order
+  union alignas(16) {
+    uint32_t out_w[kPkOut / 4 + 4];  // output staging (global alignment, zero-filled)
+    struct {                         // the length sort, done before the staging is zeroed
+      uint16_t order[kT];            // literals by ascending plaintext length
+      uint32_t hist[kBuckets];
+    };
+  };
+  uint16_t rec[kT + 1];             // literal boundaries: input byte index from the 16-B aligned start
   uint32_t rel[kT];                 // by literal: enc_len, then its range-relative output offset
-  uint16_t order[kT];               // literals by ascending plaintext length
-  uint32_t hist[kBuckets];
   uint32_t wsum[2][kT / kWave];     // per-wave totals of enc_len and capacity
   uint64_t base[2];                 // the range's place: enc and capacity bytes before it
 };
+static_assert(kPkIn + 16 < 65536, "rec holds 16-bit input indices");
+static_assert(sizeof(uint16_t) * kT + sizeof(uint32_t) * kBuckets <= sizeof(uint32_t) * (kPkOut / 4 + 4), "sort in staging");
 
 struct PackArgs {
   const uint8_t *in;
@@ -182,7 +199,7 @@ __device__ uint64_t size_literal_global(const uint8_t *src, uint64_t nbytes, con
   return bits;
 }
 
-__global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu((kT / 64 * MHQ_ENC_BLOCKS + 3) / 4))) void encode_packed_kernel(
+__global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu((kT / 64 * MHQ_PK_BLOCKS + 3) / 4))) void encode_packed_kernel(
     PackArgs a, const uint32_t *__restrict__ g_code, const uint8_t *__restrict__ g_len) {
   __shared__ PackSmem sm;
   const uint32_t tid = threadIdx.x, lane = tid % kWave, wave = tid / kWave, b = blockIdx.x;
@@ -194,15 +211,15 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu((kT / 64 * M
   for (uint32_t i = tid; i < 256u; i += kT) sm.code[i] = make_uint2(g_code[i], g_len[i]);
   const uint8_t *ia = a.in + (ib - a.in_bias);
   const uint32_t idelta = (uint32_t)((uintptr_t)ia & 15u);
-  const bool staged = (ie - ib) + idelta <= (uint64_t)kInCap;  // (uniform)
+  const bool staged = (ie - ib) + idelta <= (uint64_t)kPkIn;  // (uniform)
   if (staged) {
     const u32x4 *src = (const u32x4 *)(ia - idelta);
     // (nothing for an empty range: its aligned chunk may lie past the buffer)
     const uint32_t chunks = ie > ib ? (uint32_t)(((ie - ib) + idelta + 15u) >> 4) : 0u;
     for (uint32_t c = tid; c < chunks; c += kT)
       *(u32x4 *)(sm.in_w + 4u * c) = __builtin_nontemporal_load(src + c);  // aligned, holds a valid byte
-    if (tid == 0) sm.rec[0] = idelta;
-    if (tid < cnt) sm.rec[tid + 1] = (uint32_t)(e_t - ib) + idelta;
+    if (tid == 0) sm.rec[0] = (uint16_t)idelta;
+    if (tid < cnt) sm.rec[tid + 1] = (uint16_t)((uint32_t)(e_t - ib) + idelta);
   }
   if (tid < kBuckets) sm.hist[tid] = 0;
   __syncthreads();
@@ -268,7 +285,7 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu((kT / 64 * M
   PKTL(b, 4, tid == 0);
   // encode into the staging at the range-relative offsets (the range's
   // place in the output is not known yet: the store below realigns)
-  const bool staged_out = staged && T <= (uint32_t)kOutCap;  // (uniform)
+  const bool staged_out = staged && T <= (uint32_t)kPkOut;  // (uniform)
   if (staged_out) {
     if (tid < cnt) sm.rel[tid] = rel_e;  // (every thread read its enc_len into v above)
     for (uint32_t q = tid; q < (T + 15u) >> 4; q += kT) *(u32x4 *)(sm.out_w + 4u * q) = u32x4{0u, 0u, 0u, 0u};
