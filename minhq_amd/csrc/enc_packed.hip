@@ -52,6 +52,9 @@ __device__ unsigned long long g_pktl[kPkWgs * kPkSlots];
   } while (0)
 #endif
 
+#ifndef MHQ_PK_STG  // 1: the staging's loads all issued before its LDS stores (r05ay: config 2 -2 %)
+#define MHQ_PK_STG 1
+#endif
 #ifndef MHQ_PK_BLOCKS  // resident workgroups per CU (LDS-bound: PackSmem; 4 since r05ax: config 2 -10 %, north star -7 %)
 #define MHQ_PK_BLOCKS 4
 #endif
@@ -216,8 +219,24 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu((kT / 64 * M
     const u32x4 *src = (const u32x4 *)(ia - idelta);
     // (nothing for an empty range: its aligned chunk may lie past the buffer)
     const uint32_t chunks = ie > ib ? (uint32_t)(((ie - ib) + idelta + 15u) >> 4) : 0u;
+#if MHQ_PK_STG
+    // every load issued before the first LDS store (one HBM round trip)
+    constexpr int kSC = (kPkIn / 16 + kT - 1) / kT;
+    u32x4 v4[kSC];
+#pragma unroll
+    for (int k = 0; k < kSC; k++) {
+      const uint32_t c = tid + (uint32_t)kT * k;
+      if (c < chunks) v4[k] = __builtin_nontemporal_load(src + c);  // aligned, holds a valid byte
+    }
+#pragma unroll
+    for (int k = 0; k < kSC; k++) {
+      const uint32_t c = tid + (uint32_t)kT * k;
+      if (c < chunks) *(u32x4 *)(sm.in_w + 4u * c) = v4[k];
+    }
+#else
     for (uint32_t c = tid; c < chunks; c += kT)
       *(u32x4 *)(sm.in_w + 4u * c) = __builtin_nontemporal_load(src + c);  // aligned, holds a valid byte
+#endif
     if (tid == 0) sm.rec[0] = (uint16_t)idelta;
     if (tid < cnt) sm.rec[tid + 1] = (uint16_t)((uint32_t)(e_t - ib) + idelta);
   }
