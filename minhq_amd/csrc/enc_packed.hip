@@ -55,6 +55,12 @@ __device__ unsigned long long g_pktl[kPkWgs * kPkSlots];
 #ifndef MHQ_PK_STG  // 1: the staging's loads all issued before its LDS stores (r05ay: config 2 -2 %)
 #define MHQ_PK_STG 1
 #endif
+#ifndef MHQ_PK_SLEEP  // the look-back's back-off between polls (s_sleep units of 64 clocks)
+#define MHQ_PK_SLEEP 2
+#endif
+#ifndef MHQ_PK_SORT  // 1: a range's literals sized and encoded in length order (the waves' lanes alike)
+#define MHQ_PK_SORT 1
+#endif
 #ifndef MHQ_PK_BLOCKS  // resident workgroups per CU (LDS-bound: PackSmem; 4 since r05ax: config 2 -10 %, north star -7 %)
 #define MHQ_PK_BLOCKS 4
 #endif
@@ -142,7 +148,7 @@ __device__ void look_back(const PackArgs &a, uint32_t b, uint32_t lane, uint64_t
     for (int k = 0; k < kLbW; k++) {
       const int64_t g = hi - (int64_t)kWave * k - (int64_t)lane;
       while (g >= 0 && ((uint32_t)(ve[k] >> 34) != a.tag || (uint32_t)(vc[k] >> 34) != a.tag)) {
-        __builtin_amdgcn_s_sleep(2);
+        if (MHQ_PK_SLEEP) __builtin_amdgcn_s_sleep(MHQ_PK_SLEEP);
         ve[k] = __hip_atomic_load(sl + 2 * g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         vc[k] = __hip_atomic_load(sl + 2 * g + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
@@ -245,7 +251,7 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu((kT / 64 * M
   PKTL(b, 1, tid == 0);
   // sizing: staged, in length order (the 64 literals of a wave alike)
   uint32_t lit = tid;
-  if (staged) {
+  if (staged && MHQ_PK_SORT) {
     uint32_t bk = 0, rk = 0;
     if (tid < cnt) {
       const uint32_t bytes = sm.rec[tid + 1] - sm.rec[tid];
