@@ -61,18 +61,24 @@ __device__ unsigned long long g_pktl[kPkWgs * kPkSlots];
 #ifndef MHQ_PK_SORT  // 1: a range's literals sized and encoded in length order (the waves' lanes alike)
 #define MHQ_PK_SORT 1
 #endif
-#ifndef MHQ_PK_BLOCKS  // resident workgroups per CU (LDS-bound: PackSmem; 4 since r05ax: config 2 -10 %, north star -7 %)
-#define MHQ_PK_BLOCKS 4
+// Two shapes of the kernel, by the batch's mean literal (launch_encode_packed):
+// four resident workgroups per CU with 20,224-B plaintext and 15,360-B output
+// staging (r05ax: config 2 -10 %, north star -7 %) while a range of kT
+// literals fits the smaller staging, three with 24 / 20 KB up to the packed
+// route's 40-B bound (a range that overflows the staging takes the slow
+// per-literal global path: a 40-B mean at four ran 4.8x slower, r05bb).
+#ifndef MHQ_PK_FOUR_RANGE_BYTES  // the four-workgroup shape up to this mean range of kT literals (bytes)
+#define MHQ_PK_FOUR_RANGE_BYTES 19200
 #endif
-#ifndef MHQ_PK_INCAP  // plaintext staging (bytes)
-#define MHQ_PK_INCAP (MHQ_PK_BLOCKS >= 4 ? 20224 : MHQ_ENC_INCAP)
-#endif
-#ifndef MHQ_PK_OUTCAP  // output staging (bytes)
-#define MHQ_PK_OUTCAP (MHQ_PK_BLOCKS >= 4 ? 15360 : MHQ_ENC_OUTCAP)
-#endif
-constexpr int kPkIn = MHQ_PK_INCAP, kPkOut = MHQ_PK_OUTCAP;
+template <int kB>
+struct PkShape {
+  static constexpr int kIn = kB >= 4 ? 20224 : kInCap;    // plaintext staging (bytes)
+  static constexpr int kOut = kB >= 4 ? 15360 : kOutCap;  // output staging (bytes)
+};
 
+template <int kB>
 struct alignas(16) PackSmem {
+  static constexpr int kPkIn = PkShape<kB>::kIn, kPkOut = PkShape<kB>::kOut;
   uint2 code[256];                  // (code right-justified, length)
   uint32_t in_w[kPkIn / 4 + 4];     // plaintext, natural byte order
   union alignas(16) {
@@ -86,9 +92,10 @@ struct alignas(16) PackSmem {
   uint32_t rel[kT];                 // by literal: enc_len, then its range-relative output offset
   uint32_t wsum[2][kT / kWave];     // per-wave totals of enc_len and capacity
   uint64_t base[2];                 // the range's place: enc and capacity bytes before it
+  static_assert(kPkIn + 16 < 65536, "rec holds 16-bit input indices");
+  static_assert(sizeof(uint16_t) * kT + sizeof(uint32_t) * kBuckets <= sizeof(uint32_t) * (kPkOut / 4 + 4),
+                "sort in staging");
 };
-static_assert(kPkIn + 16 < 65536, "rec holds 16-bit input indices");
-static_assert(sizeof(uint16_t) * kT + sizeof(uint32_t) * kBuckets <= sizeof(uint32_t) * (kPkOut / 4 + 4), "sort in staging");
 
 struct PackArgs {
   const uint8_t *in;
@@ -208,9 +215,11 @@ __device__ uint64_t size_literal_global(const uint8_t *src, uint64_t nbytes, con
   return bits;
 }
 
-__global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu((kT / 64 * MHQ_PK_BLOCKS + 3) / 4))) void encode_packed_kernel(
+template <int kB>
+__global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu((kT / 64 * kB + 3) / 4))) void encode_packed_kernel(
     PackArgs a, const uint32_t *__restrict__ g_code, const uint8_t *__restrict__ g_len) {
-  __shared__ PackSmem sm;
+  __shared__ PackSmem<kB> sm;
+  constexpr int kPkIn = PackSmem<kB>::kPkIn, kPkOut = PackSmem<kB>::kPkOut;
   const uint32_t tid = threadIdx.x, lane = tid % kWave, wave = tid / kWave, b = blockIdx.x;
   PKTL(b, 0, tid == 0);
   const uint64_t n = a.n, L0 = (uint64_t)b * kT;  // (the grid is ceil(n / kT): L0 < n)
@@ -383,7 +392,8 @@ size_t encode_packed_slot_bytes(uint64_t n) { return 16u * ((n + kT - 1) / kT); 
 
 hipError_t launch_encode_packed(const DevTables &t, const uint8_t *in, const uint64_t *in_off, uint64_t in_bias,
                                 uint64_t n, uint64_t base, uint32_t *enc_len, uint64_t *out_off, uint64_t *cap_off,
-                                uint8_t *out, uint64_t out_cap, uint64_t *slots, uint64_t gen, hipStream_t s) {
+                                uint8_t *out, uint64_t out_cap, uint64_t *slots, uint64_t gen, hipStream_t s,
+                                uint64_t in_bytes) {
   if (n == 0) {
     set_base_kernel<<<1, 1, 0, s>>>(out_off, cap_off, base);
     return hipGetLastError();
@@ -391,7 +401,10 @@ hipError_t launch_encode_packed(const DevTables &t, const uint8_t *in, const uin
   const unsigned grid = (unsigned)((n + kT - 1) / kT);
   PackArgs a{in, in_off, in_bias, n, base, enc_len, out_off, cap_off, out, out_cap, slots,
              (uint32_t)(gen % 0x3fffffffull) + 1u};
-  encode_packed_kernel<<<dim3(grid), dim3(kT), 0, s>>>(a, t.code, t.len);
+  if (in_bytes * (uint64_t)kT <= (uint64_t)MHQ_PK_FOUR_RANGE_BYTES * n)
+    encode_packed_kernel<4><<<dim3(grid), dim3(kT), 0, s>>>(a, t.code, t.len);
+  else
+    encode_packed_kernel<3><<<dim3(grid), dim3(kT), 0, s>>>(a, t.code, t.len);
   return hipGetLastError();
 }
 

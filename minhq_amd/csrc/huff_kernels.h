@@ -43,7 +43,8 @@ hipError_t launch_encode(const DevTables &t, const uint8_t *in, const uint64_t *
 size_t encode_packed_slot_bytes(uint64_t n);
 hipError_t launch_encode_packed(const DevTables &t, const uint8_t *in, const uint64_t *in_off, uint64_t in_bias,
                                 uint64_t n, uint64_t base, uint32_t *enc_len, uint64_t *out_off, uint64_t *cap_off,
-                                uint8_t *out, uint64_t out_cap, uint64_t *slots, uint64_t gen, hipStream_t s);
+                                uint8_t *out, uint64_t out_cap, uint64_t *slots, uint64_t gen, hipStream_t s,
+                                uint64_t in_bytes);
 // in_end (optional): literal i is in[in_off[i] - in_bias .. e_i - in_bias), e_i
 // the first position at or after in_off[i] whose low 32 bits are in_end[i]
 // (literals under 4 GiB); e_i <= in_off[i + 1] when the literals are in order

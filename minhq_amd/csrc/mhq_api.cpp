@@ -670,7 +670,7 @@ int mhq_huff_encode_packed_dev(mhq_ctx *ctx, int dev, const uint8_t *in, const u
       static std::atomic<uint64_t> g_gen{0};
       const uint64_t gen = g_gen.fetch_add(1, std::memory_order_relaxed) + 1;
       return hip_rc(mhq::launch_encode_packed(d->tables, in, in_off, 0, n, base, enc_len, out_off, cap_off, out,
-                                              out_cap, (uint64_t *)slots.p, gen, s));
+                                              out_cap, (uint64_t *)slots.p, gen, s, in_bytes));
     }
   }
   const int rc = mhq_huff_encode_layout_dev(ctx, dev, in, in_off, n, base, enc_len, out_off, cap_off, stream);

@@ -55,8 +55,10 @@ def _run(codec, oracle_mod, data, off, base=0, with_cap=True, stream=None):
     assert got[: int(eoff[-1])].tobytes() == ref_enc.tobytes()
 
 
-@pytest.mark.parametrize("shape", ["northstar", "config2", "print", "qif_short", "odd_n"])
+@pytest.mark.parametrize("shape", ["northstar", "config2", "print", "qif_short", "odd_n", "mean37", "mean40"])
 def test_packed_short_shapes(codec, oracle_mod, shape):
+    """mean37: the four-workgroup shape's largest means (ranges of 19-20 KB in
+    its 20,224-B staging); mean40: the three-workgroup shape (24-KB staging)."""
     from minhq_amd import workloads as w
 
     if shape == "northstar":
@@ -67,8 +69,17 @@ def test_packed_short_shapes(codec, oracle_mod, shape):
         b = w.config2(1 << 16, "print")
     elif shape == "qif_short":
         b = w.make_batch(50000, "uniform", "hdr", 41, 0, 26)
+    elif shape == "mean37":
+        b = w.make_batch(1 << 16, "uniform", "hdr", 43, 30, 44)
+    elif shape == "mean40":
+        b = w.make_batch(1 << 16, "uniform", "hdr", 44, 24, 56)
     else:
         b = w.make_batch(512 * 37 + 311, "uniform", "hdr", 42, 0, 70)
+    mean = int(b.off[-1] - b.off[0]) / max(b.n, 1)
+    if shape == "mean37":
+        assert 36.0 <= mean <= 37.5, mean
+    if shape == "mean40":
+        assert 37.5 < mean <= 40.0, mean
     _run(codec, oracle_mod, b.data, b.off)
 
 
