@@ -55,6 +55,9 @@ __device__ unsigned long long g_pktl[kPkWgs * kPkSlots];
 #ifndef MHQ_PK_STG  // 1: the staging's loads all issued before its LDS stores (r05ay: config 2 -2 %)
 #define MHQ_PK_STG 1
 #endif
+#ifndef MHQ_PK_GW  // 1: unstaged ranges read their literals as aligned dwords (size_literal_global, encode_literal_global)
+#define MHQ_PK_GW 1
+#endif
 #ifndef MHQ_PK_SLEEP  // the look-back's back-off between polls (s_sleep units of 64 clocks)
 #define MHQ_PK_SLEEP 2
 #endif
@@ -211,7 +214,16 @@ __device__ __forceinline__ void store_out_shifted(uint8_t *o_al, const uint32_t 
 // Code bits of global bytes [src, src + nbytes) (a range too large to stage).
 __device__ uint64_t size_literal_global(const uint8_t *src, uint64_t nbytes, const uint2 *code) {
   uint64_t bits = 0;
-  for (uint64_t i = 0; i < nbytes; i++) bits += code[src[i]].y;
+  const uint8_t *p = src, *e = src + nbytes;
+#if MHQ_PK_GW
+  // whole aligned dwords between a byte-wise head and tail
+  for (; p < e && ((uintptr_t)p & 3u); p++) bits += code[*p].y;
+  for (; p + 4 <= e; p += 4) {
+    const uint32_t w = *(const uint32_t *)p;
+    bits += code[w & 0xffu].y + code[(w >> 8) & 0xffu].y + code[(w >> 16) & 0xffu].y + code[w >> 24].y;
+  }
+#endif
+  for (; p < e; p++) bits += code[*p].y;
   return bits;
 }
 

@@ -72,6 +72,9 @@ __device__ __forceinline__ bool thread_form(uint64_t bytes, uint64_t n) {
 #ifndef MHQ_ENC_QUAD  // the thread kernel puts a staged word's four codes at once when they fit 32 bits
 #define MHQ_ENC_QUAD 1
 #endif
+#ifndef MHQ_ENC_GW  // 1: literals encoded straight from global memory read aligned dwords (encode_literal_global)
+#define MHQ_ENC_GW 1
+#endif
 #ifndef MHQ_ENC_ALIGN  // the thread kernel's LDS alignment (16: its 16-B LDS accesses are single ds_*_b128)
 #define MHQ_ENC_ALIGN 16
 #endif
@@ -153,8 +156,26 @@ __device__ void encode_literal_global(const uint8_t *src, uint64_t nbytes, uint8
                                       uint32_t *enc_len) {
   uint64_t bits = 0;
   BitOutGlobal bo{dst, 0, 0};
-  for (uint64_t i = 0; i < nbytes; i++) {
-    const uint2 c = code[src[i]];
+  const uint8_t *p = src, *e = src + nbytes;
+#if MHQ_ENC_GW
+  // whole aligned dwords between a byte-wise head and tail
+  for (; p < e && ((uintptr_t)p & 3u); p++) {
+    const uint2 c = code[*p];
+    bits += c.y;
+    if (kEmit) bo.put(c.x, c.y);
+  }
+  for (; p + 4 <= e; p += 4) {
+    const uint32_t w = *(const uint32_t *)p;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const uint2 c = code[(w >> (8 * k)) & 0xffu];
+      bits += c.y;
+      if (kEmit) bo.put(c.x, c.y);
+    }
+  }
+#endif
+  for (; p < e; p++) {
+    const uint2 c = code[*p];
     bits += c.y;
     if (kEmit) bo.put(c.x, c.y);
   }
