@@ -64,12 +64,15 @@ __device__ unsigned long long g_pktl[kPkWgs * kPkSlots];
 #ifndef MHQ_PK_SORT  // 1: a range's literals sized and encoded in length order (the waves' lanes alike)
 #define MHQ_PK_SORT 1
 #endif
-// Two shapes of the kernel, by the batch's mean literal (launch_encode_packed):
+// Shapes of the kernel, by the batch's mean literal (launch_encode_packed):
 // four resident workgroups per CU with 20,224-B plaintext and 15,360-B output
-// staging (r05ax: config 2 -10 %, north star -7 %) while a range of kT
-// literals fits the smaller staging, three with 24 / 20 KB up to the packed
-// route's 40-B bound (a range that overflows the staging takes the slow
-// per-literal global path: a 40-B mean at four ran 4.8x slower, r05bb).
+// staging (r05ax: config 2 -10 %, north star -7 %), ranges of kT literals
+// while such a range fits the staging and of kShortR = 448 above that, to the
+// packed route's 40-B bound (r05bh: -4 to -5 % against three workgroups with
+// 24 / 20 KB and 512-literal ranges; a range that overflows the staging takes
+// the slow per-literal global path: a 40-B mean in 512-literal ranges at four
+// ran 4.8x slower, r05bb).  The three-workgroup shape remains for means past
+// 42.9 B (none on the packed route) and MHQ_PK_SHORT_R=0 builds.
 #ifndef MHQ_PK_FOUR_RANGE_BYTES  // the four-workgroup shape up to this mean range of kT literals (bytes)
 #define MHQ_PK_FOUR_RANGE_BYTES 19200
 #endif
@@ -110,6 +113,7 @@ struct PackArgs {
   uint64_t out_cap;
   uint64_t *slots;  // 2 per workgroup: enc and capacity, pack_slot()
   uint32_t tag;     // the call's look-back tag: 30 bits, never 0
+  uint32_t R;       // literals per range: kT, or kShortR (launch_encode_packed)
 };
 
 // A look-back slot: [63:34] the call's tag, [33:32] 1 aggregate / 2
@@ -234,8 +238,8 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu((kT / 64 * k
   constexpr int kPkIn = PackSmem<kB>::kPkIn, kPkOut = PackSmem<kB>::kPkOut;
   const uint32_t tid = threadIdx.x, lane = tid % kWave, wave = tid / kWave, b = blockIdx.x;
   PKTL(b, 0, tid == 0);
-  const uint64_t n = a.n, L0 = (uint64_t)b * kT;  // (the grid is ceil(n / kT): L0 < n)
-  const uint32_t cnt = (uint32_t)min((uint64_t)kT, n - L0);
+  const uint64_t n = a.n, L0 = (uint64_t)b * a.R;  // (the grid is ceil(n / R): L0 < n)
+  const uint32_t cnt = (uint32_t)min((uint64_t)a.R, n - L0);
   const uint64_t ib = uniform64(vload(a.in_off, L0)), ie = uniform64(vload(a.in_off, L0 + cnt));
   const uint64_t e_t = a.in_off[L0 + min(tid, cnt - 1u) + 1u];  // this thread's literal's end
   for (uint32_t i = tid; i < 256u; i += kT) sm.code[i] = make_uint2(g_code[i], g_len[i]);
@@ -400,7 +404,14 @@ extern "C" int mhq_diag_pktimeline(unsigned long long *out, int n) {
 }
 #endif
 
-size_t encode_packed_slot_bytes(uint64_t n) { return 16u * ((n + kT - 1) / kT); }
+#ifndef MHQ_PK_SHORT_R  // the four-workgroup shape's shorter ranges for means past MHQ_PK_FOUR_RANGE_BYTES / kT (0: none)
+#define MHQ_PK_SHORT_R 448
+#endif
+constexpr uint32_t kShortR = MHQ_PK_SHORT_R ? MHQ_PK_SHORT_R : kT;
+static_assert(kShortR <= (uint32_t)kT && kShortR % kWave == 0, "range size");
+
+// (for either range size)
+size_t encode_packed_slot_bytes(uint64_t n) { return 16u * ((n + kShortR - 1) / kShortR); }
 
 hipError_t launch_encode_packed(const DevTables &t, const uint8_t *in, const uint64_t *in_off, uint64_t in_bias,
                                 uint64_t n, uint64_t base, uint32_t *enc_len, uint64_t *out_off, uint64_t *cap_off,
@@ -410,10 +421,15 @@ hipError_t launch_encode_packed(const DevTables &t, const uint8_t *in, const uin
     set_base_kernel<<<1, 1, 0, s>>>(out_off, cap_off, base);
     return hipGetLastError();
   }
-  const unsigned grid = (unsigned)((n + kT - 1) / kT);
+  // four workgroups per CU while a mean range fits MHQ_PK_FOUR_RANGE_BYTES:
+  // ranges of kT literals, or of kShortR for a larger mean; three otherwise
+  const uint64_t fit = (uint64_t)MHQ_PK_FOUR_RANGE_BYTES * n;
+  const bool four = in_bytes * (uint64_t)kShortR <= fit;
+  const uint32_t R = four && in_bytes * (uint64_t)kT > fit ? kShortR : (uint32_t)kT;
+  const unsigned grid = (unsigned)((n + R - 1) / R);
   PackArgs a{in, in_off, in_bias, n, base, enc_len, out_off, cap_off, out, out_cap, slots,
-             (uint32_t)(gen % 0x3fffffffull) + 1u};
-  if (in_bytes * (uint64_t)kT <= (uint64_t)MHQ_PK_FOUR_RANGE_BYTES * n)
+             (uint32_t)(gen % 0x3fffffffull) + 1u, R};
+  if (four)
     encode_packed_kernel<4><<<dim3(grid), dim3(kT), 0, s>>>(a, t.code, t.len);
   else
     encode_packed_kernel<3><<<dim3(grid), dim3(kT), 0, s>>>(a, t.code, t.len);

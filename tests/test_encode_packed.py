@@ -57,8 +57,8 @@ def _run(codec, oracle_mod, data, off, base=0, with_cap=True, stream=None):
 
 @pytest.mark.parametrize("shape", ["northstar", "config2", "print", "qif_short", "odd_n", "mean37", "mean40"])
 def test_packed_short_shapes(codec, oracle_mod, shape):
-    """mean37: the four-workgroup shape's largest means (ranges of 19-20 KB in
-    its 20,224-B staging); mean40: the three-workgroup shape (24-KB staging)."""
+    """mean37: the four-workgroup shape's largest mean for 512-literal ranges
+    (19-20 KB in its 20,224-B staging); mean40: its 448-literal ranges."""
     from minhq_amd import workloads as w
 
     if shape == "northstar":
