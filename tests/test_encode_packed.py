@@ -148,6 +148,19 @@ def test_packed_tiny_batches(codec, oracle_mod):
         _run(codec, oracle_mod, data, off)
 
 
+@pytest.mark.parametrize("n", [1, 447, 448, 449, 895, 896, 3 * 448 + 17, 100003])
+def test_packed_short_ranges_edges(codec, oracle_mod, n):
+    """Means of 38-40 B take 448-literal ranges: batches at and around its
+    multiples, partial last ranges, one literal."""
+    from minhq_amd import workloads as w
+
+    b = w.make_batch(n, "uniform", "hdr", 45 + n % 7, 34, 44)
+    mean = int(b.off[-1] - b.off[0]) / max(b.n, 1)
+    if n >= 447:
+        assert 37.5 < mean <= 40.0, mean
+    _run(codec, oracle_mod, b.data, b.off, base=7)
+
+
 def test_packed_repeated_calls_two_streams(codec, oracle_mod):
     """Calls back to back on one stream (the stream's look-back slots hold the
     previous call's tags) and alternating over two streams."""
