@@ -61,11 +61,11 @@ __device__ unsigned long long g_pktl[kPkWgs * kPkSlots];
 #ifndef MHQ_PK_SLEEP  // the look-back's back-off between polls (s_sleep units of 64 clocks)
 #define MHQ_PK_SLEEP 2
 #endif
-#ifndef MHQ_PK_EARLY_LEN  // 1: enc_len stored right after the range's scan
+#ifndef MHQ_PK_EARLY_LEN  // 1: enc_len stored right after the range's scan (r05bk: +1 to +3 %)
 #define MHQ_PK_EARLY_LEN 0
 #endif
-#ifndef MHQ_PK_NT_OFF  // 1: out_off / cap_off as streaming stores
-#define MHQ_PK_NT_OFF 0
+#ifndef MHQ_PK_NT_OFF  // 1: out_off / cap_off as streaming stores (r05bk: -2 to -4 %)
+#define MHQ_PK_NT_OFF 1
 #endif
 #ifndef MHQ_PK_SORT  // 1: a range's literals sized and encoded in length order (the waves' lanes alike)
 #define MHQ_PK_SORT 1
