@@ -1,0 +1,13 @@
+#!/bin/bash
+# Round 5 evidence (final code, streaming offset stores in the packed encode): GPU suite, smoke, decode PMC (north star, config 5 long form), round_profile.
+set -o pipefail
+OUT=${1:-gpurun_out/r05final10}
+mkdir -p "$OUT"
+timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider \
+  > "$OUT/gpu_tests.txt" 2>&1 || { tail -30 "$OUT/gpu_tests.txt"; exit 1; }
+tail -1 "$OUT/gpu_tests.txt"
+timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > "$OUT/smoke.txt" 2>&1 || { tail "$OUT/smoke.txt"; exit 1; }
+tail -1 "$OUT/smoke.txt"
+bash tools/prof_pmc_lds.sh "$OUT/pmc_ns" -- python3 tools/kernel_driver.py --kernel decode --config northstar --iters 10 || exit 1
+python3 tools/pmc_summary.py "$OUT/pmc_ns" decode_kernel > "$OUT/pmc_ns_summary.txt"
+bash tools/round_profile.sh "$OUT/round"
