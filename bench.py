@@ -144,7 +144,7 @@ class Slot:
         self.enc_off = torch.empty(n + 1, dtype=torch.int64, device=dev)
         self.cap_off = torch.empty(n + 1, dtype=torch.int64, device=dev)
         # (the packed encode wants room for the most any plaintext encodes to)
-        self.enc = torch.empty(max(enc_bytes + 16, (30 * batch.nbytes + 7) // 8 if packed else 0), dtype=torch.uint8,
+        self.enc = torch.empty(max(enc_bytes + 16, 30 * batch.nbytes // 8 + batch.n if packed else 0), dtype=torch.uint8,
                                device=dev)
         self.out = torch.empty(cap_bytes + 16, dtype=torch.uint8, device=dev)
         self.out_len = torch.empty(n, dtype=torch.int32, device=dev)

@@ -126,9 +126,11 @@ int mhq_huff_encode_layout_dev(mhq_ctx *ctx, int dev, const uint8_t *in, const u
 /* The encode side of a batch in one call: enc_len[i], out_off (from base,
  * n+1 entries), cap_off (may be NULL) as mhq_huff_encode_layout_dev writes
  * them, and the encodings as mhq_huff_encode_dev writes them, literal i at
- * out[out_off[i] - base].  in_bytes must be in_off[n] - in_off[0]; out_cap (out's
- * size) must be at least (30 * in_bytes + 7) / 8, the most any plaintext
- * encodes to (MHQ_EINVAL otherwise).  A batch of short literals (mean up to
+ * out[out_off[i] - base].  in_bytes must be in_off[n] - in_off[0] (the
+ * device checks: a batch whose offsets disagree is not encoded and gets
+ * out_off[n] = UINT64_MAX); out_cap (out's size in bytes) must be at least
+ * 30 * in_bytes / 8 + n, the most any n literals of in_bytes plaintext
+ * bytes encode to (each pads to whole bytes), MHQ_EINVAL otherwise.  A batch of short literals (mean up to
  * 40 bytes, under 2^29 bytes) takes ONE launch that stages each range of
  * literals once: sized, placed by a look-back over the ranges before it,
  * encoded (enc_packed.hip); other batches take the layout call and the
@@ -155,6 +157,20 @@ int mhq_huff_decode_dev(mhq_ctx *ctx, int dev, const uint8_t *in, const uint64_t
 int mhq_huff_decode_sized_dev(mhq_ctx *ctx, int dev, const uint8_t *in, const uint64_t *in_off, uint64_t n,
                               uint64_t in_bytes, uint8_t *out, const uint64_t *out_off, uint32_t *out_len,
                               uint8_t *status, void *stream);
+/* Tuning and test hook (no reference counterpart): the kernel form of the
+ * plain batch decode (mhq_huff_decode*, not the framed strings).
+ * MHQ_DECODE_AUTO: the per-wave tile kernel (huff_decode.hip), or the
+ * long-literal kernel when in_bytes shows a mean over 64 encoded bytes;
+ * MHQ_DECODE_TILE: the tile kernel for every batch;
+ * MHQ_DECODE_STREAM: the streamed decode (huff_decode_stream.hip) for every
+ * batch.  Results are the
+ * same in every form.  Process-wide; returns the previous form, or
+ * MHQ_EINVAL for an unknown one.  MHQ_DECODE_FORM=auto|tile|stream in the
+ * environment sets the initial form. */
+#define MHQ_DECODE_AUTO 0
+#define MHQ_DECODE_TILE 1
+#define MHQ_DECODE_STREAM 2
+int mhq_set_decode_form(int form);
 
 /* ---------------- string literals: H bit + prefix integer + payload --------
  * Batch Reader.ReadString(prefix) and Writer.WriteStringRaw(s, prefix, choice)

@@ -32,6 +32,9 @@ MHQ_VARINT_OK = 0
 MHQ_VARINT_EOF = 1
 MHQ_VARINT_TOO_LARGE = 2
 MHQ_VARINT_NOSPACE = 3
+MHQ_DECODE_AUTO = 0
+MHQ_DECODE_TILE = 1
+MHQ_DECODE_STREAM = 2
 
 u8p = C.POINTER(C.c_uint8)
 u32p = C.POINTER(C.c_uint32)
@@ -60,6 +63,7 @@ SIGNATURES = {
     "mhq_huff_encode_dev": (C.c_int, [vp, C.c_int, vp, vp, C.c_uint64, vp, vp, vp]),
     "mhq_huff_decode_dev": (C.c_int, [vp, C.c_int, vp, vp, C.c_uint64, vp, vp, vp, vp, vp]),
     "mhq_huff_decode_sized_dev": (C.c_int, [vp, C.c_int, vp, vp, C.c_uint64, C.c_uint64, vp, vp, vp, vp, vp]),
+    "mhq_set_decode_form": (C.c_int, [C.c_int]),
     "mhq_read_strings_dev": (C.c_int, [vp, C.c_int, vp, C.c_uint64, vp, vp, vp, C.c_uint64, vp, C.c_uint64,
                                        vp, vp, vp, vp, vp]),
     "mhq_write_strings_dev": (C.c_int, [vp, C.c_int, vp, vp, C.c_uint64, vp, vp, C.c_int, vp, C.c_uint64,

@@ -12,7 +12,7 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libmhq_huff.so")
-SOURCES = ["huff_decode.hip", "read_strings.hip", "huff_encode.hip", "enc_packed.hip", "huff_scan.hip", "str_frame.hip", "huff_table.cpp", "mhq_api.cpp"]
+SOURCES = ["huff_decode.hip", "huff_decode_stream.hip", "read_strings.hip", "huff_encode.hip", "enc_packed.hip", "huff_scan.hip", "str_frame.hip", "huff_table.cpp", "mhq_api.cpp"]
 HEADERS = ["huff_kernels.h", "huff_decode_dev.h", "huff_encode_dev.h", "huff_common.h", "huff_table.h", os.path.join("..", "..", "include", "mhq_huff.h")]
 ARCH = os.environ.get("MHQ_OFFLOAD_ARCH", "gfx950")
 

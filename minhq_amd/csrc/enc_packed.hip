@@ -120,6 +120,7 @@ struct PackArgs {
   uint64_t *slots;  // 2 per workgroup: enc and capacity, pack_slot()
   uint32_t tag;     // the call's look-back tag: 30 bits, never 0
   uint32_t R;       // literals per range: kT, or kShortR (launch_encode_packed)
+  uint64_t in_bytes;  // the caller's in_off[n] - in_off[0], verified by every workgroup
 };
 
 // A look-back slot: [63:34] the call's tag, [33:32] 1 aggregate / 2
@@ -246,6 +247,13 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu((kT / 64 * k
   PKTL(b, 0, tid == 0);
   const uint64_t n = a.n, L0 = (uint64_t)b * a.R;  // (the grid is ceil(n / R): L0 < n)
   const uint32_t cnt = (uint32_t)min((uint64_t)a.R, n - L0);
+  // The caller's in_bytes chose this path and bounds every look-back sum
+  // (< 2^32): a batch whose offsets say otherwise is not encoded; out_off[n]
+  // = UINT64_MAX tells the caller (include/mhq_huff.h).
+  if (uniform64(vload(a.in_off, n)) - uniform64(vload(a.in_off, 0)) != a.in_bytes) {
+    if (b == 0 && tid == 0) a.out_off[n] = ~0ull;
+    return;
+  }
   const uint64_t ib = uniform64(vload(a.in_off, L0)), ie = uniform64(vload(a.in_off, L0 + cnt));
   const uint64_t e_t = a.in_off[L0 + min(tid, cnt - 1u) + 1u];  // this thread's literal's end
   for (uint32_t i = tid; i < 256u; i += kT) sm.code[i] = make_uint2(g_code[i], g_len[i]);
@@ -431,7 +439,7 @@ size_t encode_packed_slot_bytes(uint64_t n) { return 16u * ((n + kShortR - 1) / 
 
 hipError_t launch_encode_packed(const DevTables &t, const uint8_t *in, const uint64_t *in_off, uint64_t in_bias,
                                 uint64_t n, uint64_t base, uint32_t *enc_len, uint64_t *out_off, uint64_t *cap_off,
-                                uint8_t *out, uint64_t out_cap, uint64_t *slots, uint64_t gen, hipStream_t s,
+                                uint8_t *out, uint64_t out_cap, uint64_t *slots, uint32_t tag, hipStream_t s,
                                 uint64_t in_bytes) {
   if (n == 0) {
     set_base_kernel<<<1, 1, 0, s>>>(out_off, cap_off, base);
@@ -443,8 +451,8 @@ hipError_t launch_encode_packed(const DevTables &t, const uint8_t *in, const uin
   const bool four = in_bytes * (uint64_t)kShortR <= fit;
   const uint32_t R = four && in_bytes * (uint64_t)kT > fit ? kShortR : (uint32_t)kT;
   const unsigned grid = (unsigned)((n + R - 1) / R);
-  PackArgs a{in, in_off, in_bias, n, base, enc_len, out_off, cap_off, out, out_cap, slots,
-             (uint32_t)(gen % 0x3fffffffull) + 1u, R};
+  PackArgs a{in, in_off, in_bias, n, base, enc_len, out_off, cap_off, out, out_cap, slots, (uint32_t)tag, R,
+             in_bytes};
   if (four)
     encode_packed_kernel<4><<<dim3(grid), dim3(kT), 0, s>>>(a, t.code, t.len);
   else

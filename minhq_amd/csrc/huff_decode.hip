@@ -132,6 +132,9 @@ hipError_t launch_decode(const DevTables &t, const uint8_t *in, const uint64_t *
                          uint32_t *out_len, uint8_t *status, hipStream_t s, const uint32_t *in_end,
                          const StrFinish *str, uint64_t in_bytes) {
   if (n == 0) return hipSuccess;
+  const int form = decode_form();
+  if (!in_end && form == kDecodeStream)
+    return launch_decode_stream(t, in, in_off, in_bias, n, out, out_off, out_bias, out_len, status, s);
   if (!in_end && in_bytes > (uint64_t)kLongMean * n) {  // every tile would stream: the long-literal form
     const uint64_t cus = (uint64_t)dev::device_cus();
     const uint64_t blocks = cus * MHQ_DEC_LW_BLOCKS;

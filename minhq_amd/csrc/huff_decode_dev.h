@@ -319,7 +319,11 @@ struct WinBuf3 {
 
 // One step on a window's 32 bits S (win_step32: S read from LDS at the step;
 // win_pair: from three words read for two steps).
-template <bool kLong>
+// kSafe (the streamed decode, huff_decode_stream.hip): a step that leaves
+// `left` < 0 -- a code decoded across the literal's end -- pends nothing, so
+// no byte of a malformed tail is ever OR-ed into the output (the literal is
+// then decoded again by the exact path; the stream has no piece to redo).
+template <bool kLong, bool kSafe = false>
 __device__ __forceinline__ bool win_step_s(const Smem &sm, WinBuf3 &in, uint32_t S, OutAccL &out, PendL &pend,
                                            bool &stop) {
   stop = S >= 0xfffffffcu;
@@ -342,6 +346,7 @@ __device__ __forceinline__ bool win_step_s(const Smem &sm, WinBuf3 &in, uint32_t
   in.set_mask();
   pend.p = out.op;
   pend.v = (uint32_t)out.acc;
+  if (kSafe) pend.v = in.left < 0 ? 0u : pend.v;
   const uint32_t t = out.ab & 32u;
   out.acc >>= t;
   out.op += t >> 5;
@@ -349,9 +354,9 @@ __device__ __forceinline__ bool win_step_s(const Smem &sm, WinBuf3 &in, uint32_t
   return stop || in.left < 0;
 }
 
-template <bool kLong = true>
+template <bool kLong = true, bool kSafe = false>
 __device__ __forceinline__ bool win_step32(const Smem &sm, WinBuf3 &in, OutAccL &out, PendL &pend, bool &stop) {
-  return win_step_s<kLong>(sm, in, in.top(), out, pend, stop);
+  return win_step_s<kLong, kSafe>(sm, in, in.top(), out, pend, stop);
 }
 
 // Two steps from one window read: three words from the first step's bit
@@ -359,15 +364,15 @@ __device__ __forceinline__ bool win_step32(const Smem &sm, WinBuf3 &in, OutAccL 
 // 24 bits), so the second step's window comes from registers (one LDS round
 // trip less on the step chain).  The words past a literal are the slice's
 // look-ahead slack.
-template <bool kLongB>
+template <bool kLongB, bool kSafe = false>
 __device__ __forceinline__ bool win_pair(const Smem &sm, WinBuf3 &in, OutAccL &out, PendL &pend, bool &stop) {
   typedef __attribute__((address_space(3))) const uint32_t lds_u32;
   lds_u32 *w = (lds_u32 *)(uintptr_t)((in.pm >> 3) & ~3u);
   const uint32_t k0 = in.pm >> 5, w0 = w[0], w1 = w[1], w2 = w[2];
-  win_step_s<false>(sm, in, __builtin_amdgcn_alignbit(w0, w1, ~in.pm) | in.msk, out, pend, stop);
+  win_step_s<false, kSafe>(sm, in, __builtin_amdgcn_alignbit(w0, w1, ~in.pm) | in.msk, out, pend, stop);
   const bool hi = (in.pm >> 5) != k0;
-  return win_step_s<kLongB>(sm, in, __builtin_amdgcn_alignbit(hi ? w1 : w0, hi ? w2 : w1, ~in.pm) | in.msk, out, pend,
-                            stop);
+  return win_step_s<kLongB, kSafe>(sm, in, __builtin_amdgcn_alignbit(hi ? w1 : w0, hi ? w2 : w1, ~in.pm) | in.msk, out,
+                                   pend, stop);
 }
 
 
@@ -1143,7 +1148,7 @@ __device__ MHQ_CALLEE_LONG void decode_tile_long(const SM &sm, W &ws, const uint
 // Slow path: a tile whose bytes exceed the slices, in greedy pieces staged
 // synchronously from global memory; a literal larger than a slice alone is
 // decoded by lane 0 from global memory.
-__device__ void decode_tile_pieces(const Smem &sm, WaveSmem &ws, const uint8_t *__restrict__ in,
+[[maybe_unused]] __device__ void decode_tile_pieces(const Smem &sm, WaveSmem &ws, const uint8_t *__restrict__ in,
                                    const uint64_t *__restrict__ in_off, uint64_t in_bias, uint8_t *__restrict__ out,
                                    const uint64_t *__restrict__ out_off, uint64_t out_bias,
                                    uint32_t *__restrict__ out_len, uint8_t *__restrict__ status, uint64_t s,

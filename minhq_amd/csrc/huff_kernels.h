@@ -39,11 +39,14 @@ hipError_t launch_encode(const DevTables &t, const uint8_t *in, const uint64_t *
 // launch (enc_packed.hip), for batches under 2^29 plaintext bytes: out holds
 // the encodings from out_off[0] = base on, out_cap bytes (a literal whose
 // region ends past it is not written).  slots: encode_packed_slot_bytes(n)
-// bytes that only look-backs use (a stale slot carries another call's tag).
+// bytes that only look-backs use, tag: this call's, in 1 .. 2^30 - 1, never
+// held by a slot of an earlier call on the buffer (take_slots, mhq_api.cpp).
+// in_bytes must be in_off[n] - in_off[0]: otherwise nothing is encoded and
+// out_off[n] = UINT64_MAX.
 size_t encode_packed_slot_bytes(uint64_t n);
 hipError_t launch_encode_packed(const DevTables &t, const uint8_t *in, const uint64_t *in_off, uint64_t in_bias,
                                 uint64_t n, uint64_t base, uint32_t *enc_len, uint64_t *out_off, uint64_t *cap_off,
-                                uint8_t *out, uint64_t out_cap, uint64_t *slots, uint64_t gen, hipStream_t s,
+                                uint8_t *out, uint64_t out_cap, uint64_t *slots, uint32_t tag, hipStream_t s,
                                 uint64_t in_bytes);
 // in_end (optional): literal i is in[in_off[i] - in_bias .. e_i - in_bias), e_i
 // the first position at or after in_off[i] whose low 32 bits are in_end[i]
@@ -72,6 +75,19 @@ hipError_t launch_decode(const DevTables &t, const uint8_t *in, const uint64_t *
                          uint64_t in_bias, uint64_t n, uint8_t *out, const uint64_t *out_off,
                          uint64_t out_bias, uint32_t *out_len, uint8_t *status, hipStream_t s,
                          const uint32_t *in_end = nullptr, const StrFinish *str = nullptr, uint64_t in_bytes = 0);
+// The streamed decode (huff_decode_stream.hip): launch_decode's form for the
+// plain decode (no in_end) when kDecodeStream is set.
+hipError_t launch_decode_stream(const DevTables &t, const uint8_t *in, const uint64_t *in_off, uint64_t in_bias,
+                                uint64_t n, uint8_t *out, const uint64_t *out_off, uint64_t out_bias,
+                                uint32_t *out_len, uint8_t *status, hipStream_t s);
+// Which form launch_decode takes for the plain decode: kDecodeAuto (the tile
+// kernel, or the long-literal kernel when in_bytes shows a mean over
+// kLongMean), kDecodeTile (the tile kernel, huff_decode.hip), kDecodeStream
+// (huff_decode_stream.hip).
+// Set by mhq_set_decode_form (tests, A/B runs) or MHQ_DECODE_FORM at load.
+enum DecodeForm { kDecodeAuto = 0, kDecodeTile = 1, kDecodeStream = 2 };
+int decode_form();
+int set_decode_form(int form);  // the previous form, -1 for an unknown one
 // in_bytes (the batch's encoded bytes, 0 if unknown): a mean literal over
 // kLongMean bytes takes the long-literal form (decode_long_kernel)
 #ifndef MHQ_DEC_LONG_MEAN

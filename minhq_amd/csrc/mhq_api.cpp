@@ -99,6 +99,7 @@ struct Device {
     void *p;
     size_t bytes;
     int holders;  // callers between stream_scratch and the end of their enqueueing (ScratchLease)
+    uint32_t tag = 0;  // the slots pool: the last look-back tag handed out on this buffer
   };
   std::mutex scratch_mu;
   std::vector<Scratch> scratch;
@@ -257,6 +258,29 @@ void *stream_buffer(Device *d, std::vector<Device::Scratch> &pool, hipStream_t s
   return p;
 }
 void *stream_scratch(Device *d, hipStream_t s, size_t bytes) { return stream_buffer(d, d->scratch, s, bytes); }
+
+// The packed encode's look-back slots for one call on stream s, and the
+// call's tag (1 .. 2^30 - 1).  A slot whose tag equals the call's is taken
+// as this call's, so the tags are per buffer and stream-ordered: a new
+// buffer is zeroed (tag 0 is never handed out), and when a buffer's tags
+// wrap it is zeroed again in stream order before the call that restarts at 1
+// (stale slots of an older, larger call).
+constexpr uint32_t kMaxSlotTag = (1u << 30) - 1u;
+void *take_slots(Device *d, hipStream_t s, size_t bytes, uint32_t *tag) {
+  void *p = stream_buffer(d, d->slots, s, bytes);
+  if (!p) return nullptr;
+  std::lock_guard<std::mutex> g(d->scratch_mu);
+  for (auto &x : d->slots) {
+    if (x.p != p) continue;
+    if (x.tag == 0 || x.tag >= kMaxSlotTag) {
+      if (hipMemsetAsync(p, 0, x.bytes, s) != hipSuccess) return nullptr;
+      x.tag = 0;
+    }
+    *tag = ++x.tag;
+    return p;
+  }
+  return nullptr;
+}
 
 // Ends a caller's hold on a buffer from stream_scratch (after it has
 // enqueued every use of it).
@@ -658,19 +682,21 @@ int mhq_huff_encode_packed_dev(mhq_ctx *ctx, int dev, const uint8_t *in, const u
                                uint64_t *cap_off, uint8_t *out, uint64_t out_cap, void *stream) {
   Device *d = device(ctx, dev);
   if (!d || !out_off || (n && (!in_off || !enc_len || !out))) return MHQ_EINVAL;
-  if (in_bytes > (UINT64_MAX - 7) / 30 || out_cap < (30 * in_bytes + 7) / 8) return MHQ_EINVAL;
+  // every literal pads to whole bytes: sum ceil(30 L_i / 8) <= floor(30 in_bytes / 8) + n
+  if (in_bytes > (UINT64_MAX - n) / 30 || out_cap < 30 * in_bytes / 8 + n) return MHQ_EINVAL;
   MHQ_TRY(hipSetDevice(d->ordinal));
   hipStream_t s = (hipStream_t)stream;
   // one launch for short literals (a mean <= 40 B: a range of 512 stages in 24 KB; and
   // every look-back sum under 2^32); otherwise the layout call and the
   // encode, whose forms suit long literals
   if (in_bytes < ((uint64_t)1 << 29) && in_bytes <= (uint64_t)MHQ_PK_MAX_MEAN * n) {
-    ScratchLease slots(d, d->slots, s, mhq::encode_packed_slot_bytes(n));
-    if (slots.p) {
-      static std::atomic<uint64_t> g_gen{0};
-      const uint64_t gen = g_gen.fetch_add(1, std::memory_order_relaxed) + 1;
-      return hip_rc(mhq::launch_encode_packed(d->tables, in, in_off, 0, n, base, enc_len, out_off, cap_off, out,
-                                              out_cap, (uint64_t *)slots.p, gen, s, in_bytes));
+    uint32_t tag = 0;
+    void *sp = take_slots(d, s, mhq::encode_packed_slot_bytes(n), &tag);
+    if (sp) {
+      const hipError_t e = mhq::launch_encode_packed(d->tables, in, in_off, 0, n, base, enc_len, out_off, cap_off,
+                                                     out, out_cap, (uint64_t *)sp, tag, s, in_bytes);
+      release_scratch(d, sp);
+      return hip_rc(e);
     }
   }
   const int rc = mhq_huff_encode_layout_dev(ctx, dev, in, in_off, n, base, enc_len, out_off, cap_off, stream);
@@ -703,6 +729,11 @@ int mhq_huff_decode_sized_dev(mhq_ctx *ctx, int dev, const uint8_t *in, const ui
   MHQ_TRY(hipSetDevice(d->ordinal));
   return hip_rc(mhq::launch_decode(d->tables, in, in_off, 0, n, out, out_off, 0, out_len, status,
                                    (hipStream_t)stream, nullptr, nullptr, in_bytes));
+}
+
+int mhq_set_decode_form(int form) {
+  const int prev = mhq::set_decode_form(form);
+  return prev < 0 ? MHQ_EINVAL : prev;
 }
 
 int mhq_huff_decode_dev(mhq_ctx *ctx, int dev, const uint8_t *in, const uint64_t *in_off, uint64_t n,

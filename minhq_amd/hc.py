@@ -375,8 +375,10 @@ class Codec:
     def encode_packed_dev(self, data, off, in_bytes: int, enc_len, out_off, cap_off, out, base: int = 0,
                           dev: int = 0, stream=None) -> None:
         """encode_layout_dev + encode_dev in one call (one launch for short
-        literals); out must hold (30 * in_bytes + 7) // 8 bytes."""
+        literals); out (uint8) must hold 30 * in_bytes // 8 + n bytes."""
         n = off.numel() - 1
+        if out.element_size() != 1:
+            raise TypeError("encode_packed_dev: out must be a byte tensor")
         check(self._L.mhq_huff_encode_packed_dev(self._h, dev, data.data_ptr(), off.data_ptr(), n, in_bytes, base,
                                                  enc_len.data_ptr(), out_off.data_ptr(),
                                                  cap_off.data_ptr() if cap_off is not None else None,

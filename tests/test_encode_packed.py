@@ -36,7 +36,7 @@ def _run(codec, oracle_mod, data, off, base=0, with_cap=True, stream=None):
     enc_len = torch.full((max(n, 1),), -1, dtype=torch.int32, device=dev)
     out_off = torch.full((n + 1,), -1, dtype=torch.int64, device=dev)
     cap_off = torch.full((n + 1,), -1, dtype=torch.int64, device=dev) if with_cap else None
-    cap = (30 * in_bytes + 7) // 8
+    cap = 30 * in_bytes // 8 + n  # the most n literals of in_bytes bytes encode to (include/mhq_huff.h)
     out = torch.full((max(cap, 1),), 0xA5, dtype=torch.uint8, device=dev)
     torch.cuda.synchronize()  # (the inputs' copies are on the current stream)
     codec.encode_packed_dev(t_data, t_off, in_bytes, enc_len, out_off, cap_off, out, base=base, stream=stream)
@@ -186,6 +186,65 @@ def test_packed_rejects_small_out(codec):
     in_bytes = int(b.off[-1])
     enc_len = torch.empty(1000, dtype=torch.int32, device=dev)
     out_off = torch.empty(1001, dtype=torch.int64, device=dev)
-    out = torch.empty((30 * in_bytes + 7) // 8 - 1, dtype=torch.uint8, device=dev)
+    out = torch.empty(30 * in_bytes // 8 + 1000 - 1, dtype=torch.uint8, device=dev)
     with pytest.raises(_lib.MhqError):
         codec.encode_packed_dev(t_data, t_off, in_bytes, enc_len, out_off, None, out)
+
+
+@pytest.mark.parametrize("form", ["packed", "layout"])
+def test_packed_worst_case_padding_at_min_cap(codec, oracle_mod, form):
+    """Literals made only of bytes 10, 13 and 22 (30-bit codes) pad to whole
+    bytes: n literals of L bytes need sum ceil(30 L / 8), up to
+    floor(30 in_bytes / 8) + n, more than (30 in_bytes + 7) / 8 (ADVICE r5).
+    At exactly the documented minimum out_cap every byte is written, on the
+    one-launch path (1-byte literals) and on the layout + encode path (43-byte
+    literals: a mean over 40 bytes)."""
+    from minhq_amd import hc
+
+    rng = np.random.default_rng(6)
+    L = 1 if form == "packed" else 43
+    lits = [bytes(rng.choice([10, 13, 22], size=L).astype(np.uint8)) for _ in range(3000)]
+    data, off = hc.pack(lits)
+    n = len(lits)
+    in_bytes = int(off[-1])
+    need = sum((30 * len(x) + 7) // 8 for x in lits)
+    assert (30 * in_bytes + 7) // 8 < need <= 30 * in_bytes // 8 + n
+    _run(codec, oracle_mod, data, off)
+
+
+def test_packed_in_bytes_mismatch_poisons_out_off(codec):
+    """An in_bytes that is not in_off[n] - in_off[0] is caught on the device:
+    nothing is encoded and out_off[n] is UINT64_MAX (VERDICT r5 #5)."""
+    import torch
+
+    from minhq_amd import workloads as w
+
+    b = w.north_star(5000)
+    dev = torch.device("cuda:0")
+    t_data = torch.from_numpy(b.data.copy()).to(dev)
+    t_off = torch.from_numpy(b.off.view(np.int64).copy()).to(dev)
+    in_bytes = int(b.off[-1])
+    enc_len = torch.zeros(5000, dtype=torch.int32, device=dev)
+    out_off = torch.zeros(5001, dtype=torch.int64, device=dev)
+    out = torch.full((30 * in_bytes // 8 + 5000,), 0xA5, dtype=torch.uint8, device=dev)
+    codec.encode_packed_dev(t_data, t_off, in_bytes - 100, enc_len, out_off, None, out)
+    torch.cuda.synchronize()
+    assert int(out_off[-1].item()) == -1  # UINT64_MAX
+    assert int((out != 0xA5).sum().item()) == 0
+
+
+def test_packed_stale_slots_with_next_tag(codec, oracle_mod):
+    """Look-back slots left by a larger call can never match a later call's
+    tag: the tags are per slot buffer and the buffer is zeroed when it is
+    allocated and when its tags wrap (take_slots, mhq_api.cpp).  Poison the
+    stream's slot buffer with every tag a later call could use -- here, by
+    running many calls of different sizes on one stream, the small ones
+    after large ones -- and check each against the oracle."""
+    import torch
+
+    from minhq_amd import workloads as w
+
+    s = torch.cuda.Stream()
+    for n in (20000, 300, 9000, 77, 20000, 5, 1500):
+        b = w.north_star(n)
+        _run(codec, oracle_mod, b.data, b.off, stream=s)

@@ -8,7 +8,7 @@ SRC=minhq_amd/csrc
 build_one() {
   name=${1%%=*}; flags=${1#*=}
   hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared $flags -o "$OUT/lib_$name.so" \
-    $SRC/huff_decode.hip $SRC/read_strings.hip $SRC/huff_encode.hip $SRC/enc_packed.hip $SRC/huff_scan.hip $SRC/str_frame.hip $SRC/huff_table.cpp $SRC/mhq_api.cpp \
+    $SRC/huff_decode.hip $SRC/huff_decode_stream.hip $SRC/read_strings.hip $SRC/huff_encode.hip $SRC/enc_packed.hip $SRC/huff_scan.hip $SRC/str_frame.hip $SRC/huff_table.cpp $SRC/mhq_api.cpp \
     > "$OUT/build_$name.log" 2>&1 && echo "built $name" || { echo "FAILED $name"; tail -5 "$OUT/build_$name.log"; }
 }
 export -f build_one; export OUT SRC
