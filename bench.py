@@ -5,8 +5,11 @@ Metric (BASELINE.json): "device-resident Huffman literal GiB/s (encode+decode)".
 Workload (BASELINE.json configs[1]): 2^20 synthetic header-field literals per
 GPU, lengths U{8..64}, bytes drawn from the netbsd.qif header-byte histogram
 (minhq_amd/workloads.py).  One step = one full round trip of
-one batch on the device: encode_len -> offsets scan -> encode -> decode, all
-through the C ABI (include/mhq_huff.h), inputs resident in HBM.  Rotating
+one batch on the device: the packed encode (sizes, offsets and codes in one
+launch, mhq_huff_encode_packed_dev) then the decode (mhq_huff_decode_dev),
+both through the C ABI (include/mhq_huff.h), inputs resident in HBM; the two
+calls of each slot are bound once (hc.Codec.bound_call), so the host pays per
+step about what a cgo caller would, not ctypes' argument conversion.  Rotating
 copies of every buffer (>= 1 GiB in all) keep the 256 MB Infinity Cache from
 serving a step's inputs from the previous step.
 
@@ -22,7 +25,8 @@ owns an independent batch (no data-path collective, weak scaling); the
 process group carries only the barrier and the max over ranks.
 
 Extra fields (not `value`):
-  roofline            the dominant kernel (decode) against the HBM roofline;
+  roofline            the step's dominant (longest) kernel against the HBM
+                      roofline; roofline_decode / roofline_encode_packed: both;
   long_run            the same step timed over >= 200 steps;
   decode_only_northstar  2^20 x U{8..56} decode (the north star's shape);
   config4_sharded     one 2^24-literal Zipf batch (BASELINE.json configs[3]),
@@ -169,7 +173,21 @@ def encoded_sizes(codec, batch, dev):
 PACKED = True  # --encode packed: the encode side as one call (mhq_huff_encode_packed_dev)
 
 
-def round_trip(codec, s, stream=None):
+def bind_round_trip(codec, s, stream=None):
+    """The step's two calls (packed encode, decode) on slot s, bound once
+    (hc.Codec.bound_call): the timed loop then pays a cgo-like host cost per
+    call, not ctypes' conversion of a dozen arguments (the
+    20-step run lost 14 % to submission)."""
+    return (codec.bind_encode_packed_dev(s.data, s.off, s.plain, s.enc_len, s.enc_off, s.cap_off, s.enc,
+                                         stream=stream),
+            codec.bind_decode_dev(s.enc, s.enc_off, s.out, s.cap_off, s.out_len, s.status, stream=stream))
+
+
+def round_trip(codec, s, stream=None, bound=None):
+    if bound is not None:
+        for call in bound:
+            call()
+        return
     if PACKED:
         # sizes, placement and codes in one launch (enc_packed.hip), decode
         codec.encode_packed_dev(s.data, s.off, s.plain, s.enc_len, s.enc_off, s.cap_off, s.enc, stream=stream)
@@ -741,14 +759,16 @@ def main():
         for s in slots:
             round_trip(codec, s)
             verify_slot(s)
+    # slot i % R always runs on stream i % S (R is a multiple of S): its calls bound once
+    bound = [bind_round_trip(codec, slots[i], streams[i % S]) if PACKED else None for i in range(R)]
     for i in range(args.warmup):
-        round_trip(codec, slots[i % R], streams[i % S])
+        round_trip(codec, slots[i % R], streams[i % S], bound[i % R])
     # the timed region: K whole steps, no instrumentation between the kernels
     # (a timing event between two launches costs ~5.7 us of idle GPU)
     barrier(pg)
     t0 = time.perf_counter()
     for i in range(args.steps):
-        round_trip(codec, slots[i % R], streams[i % S])
+        round_trip(codec, slots[i % R], streams[i % S], bound[i % R])
     barrier(pg)
     el = time.perf_counter() - t0
     el_max = max_over_ranks(pg, el)
@@ -759,7 +779,7 @@ def main():
         barrier(pg)
         t0 = time.perf_counter()
         for i in range(args.long_steps):
-            round_trip(codec, slots[i % R], streams[i % S])
+            round_trip(codec, slots[i % R], streams[i % S], bound[i % R])
         barrier(pg)
         el_long = max_over_ranks(pg, time.perf_counter() - t0)
         for s in slots:

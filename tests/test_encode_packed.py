@@ -244,7 +244,7 @@ def test_packed_stale_slots_with_next_tag(codec, oracle_mod):
 
     from minhq_amd import workloads as w
 
-    s = torch.cuda.Stream()
+    s = torch.cuda.Stream().cuda_stream
     for n in (20000, 300, 9000, 77, 20000, 5, 1500):
         b = w.north_star(n)
         _run(codec, oracle_mod, b.data, b.off, stream=s)
