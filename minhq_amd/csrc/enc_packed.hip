@@ -61,9 +61,6 @@ __device__ unsigned long long g_pktl[kPkWgs * kPkSlots];
 #ifndef MHQ_PK_SLEEP  // the look-back's back-off between polls (s_sleep units of 64 clocks)
 #define MHQ_PK_SLEEP 2
 #endif
-#ifndef MHQ_PK_EARLY_LEN  // 1: enc_len stored right after the range's scan (r05bk: +1 to +3 %)
-#define MHQ_PK_EARLY_LEN 0
-#endif
 #ifndef MHQ_PK_NT_OFF  // 1: out_off / cap_off as streaming stores (r05bk: -2 to -4 %)
 #define MHQ_PK_NT_OFF 1
 #endif
@@ -338,9 +335,6 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu((kT / 64 * k
     C += sm.wsum[1][w];
   }
   const uint32_t rel_e = be + ve - v, rel_c = bc + vc - c;
-#if MHQ_PK_EARLY_LEN  // enc_len needs no base: stored before the encode and the look-back
-  if (tid < cnt) __builtin_nontemporal_store(v, a.enc_len + L0 + tid);
-#endif
   // publish the range's totals at once, so that the ranges after it can
   // add them up while this one encodes
   if (tid == 0) {
@@ -381,9 +375,7 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu((kT / 64 * k
   PKTL(b, 7, tid == 0);
   const uint64_t base_e = sm.base[0], base_c = sm.base[1];
   if (tid < cnt) {
-#if !MHQ_PK_EARLY_LEN
     __builtin_nontemporal_store(v, a.enc_len + L0 + tid);
-#endif
 #if MHQ_PK_NT_OFF
     __builtin_nontemporal_store(a.base + base_e + rel_e, a.out_off + L0 + tid);
     if (a.cap_off) __builtin_nontemporal_store(a.base + base_c + rel_c, a.cap_off + L0 + tid);

@@ -183,6 +183,36 @@ __device__ __forceinline__ void store_out(uint8_t *o_al, const uint8_t *lds, uin
   if (lane < 32 && x < (lane < 16 ? head_end : hi)) o_al[x] = lds[x];
 }
 
+// store_out for a slice of at most kMax wave-wide rounds of whole chunks
+// (kMax * 64 * 16 bytes): every LDS read is issued before the first global
+// store, so the copy waits for one LDS round trip, not one per round (the
+// loop form waits after each ds_read_b128; under the probe loops' LDS load a
+// round trip is hundreds of cycles).  Reads past the last whole chunk re-read
+// it (no branch around a read); only the stores are predicated.
+template <int kMax>
+__device__ __forceinline__ void store_out_batched(uint8_t *o_al, const uint8_t *lds, uint32_t lo, uint32_t hi,
+                                                  int lane) {
+  if (hi <= lo) return;
+  CRUMB(40, o_al + hi - 1);
+  const uint32_t f0 = (lo + 15u) >> 4, f1 = hi >> 4;  // whole chunks [f0, f1)
+  if (f1 > f0) {
+    u32x4 v[kMax];
+#pragma unroll
+    for (int k = 0; k < kMax; k++) {
+      const uint32_t c = min(f0 + (uint32_t)lane + (uint32_t)(kWave * k), f1 - 1u);
+      v[k] = *(const u32x4 *)(lds + (c << 4));
+    }
+#pragma unroll
+    for (int k = 0; k < kMax; k++) {
+      const uint32_t c = f0 + (uint32_t)lane + (uint32_t)(kWave * k);
+      if (c < f1) __builtin_nontemporal_store(v[k], (u32x4 *)(o_al + (c << 4)));
+    }
+  }
+  const uint32_t head_end = min(hi, f0 << 4), tail_start = max(head_end, f1 << 4);
+  const uint32_t x = lane < 16 ? lo + (uint32_t)lane : tail_start + (uint32_t)lane - 16u;
+  if (lane < 32 && x < (lane < 16 ? head_end : hi)) o_al[x] = lds[x];
+}
+
 __device__ __forceinline__ uint32_t lds_byte(const uint32_t *w, uint32_t x) {
   return (w[x >> 2] >> ((x & 3u) * 8u)) & 0xffu;
 }

@@ -26,16 +26,12 @@
 #ifndef MHQ_DEC_STEPS_GAPS  // the same for the in_end decode of framed strings (read_strings; 3 since r05j: -1..-4 %)
 #define MHQ_DEC_STEPS_GAPS 3
 #endif
-// The decode's out-of-line helpers (the checked loop, the streamed long
-// literals, the head repair): called functions, or inlined where they are
-// used (-DMHQ_DEC_INLINE_CALLS=1, an experiment)
-#if defined(MHQ_DEC_INLINE_CALLS) && MHQ_DEC_INLINE_CALLS
-#define MHQ_CALLEE __forceinline__
-#define MHQ_CALLEE_LONG __forceinline__
-#else
+// The decode's out-of-line helper (the checked loop) is a called function;
+// the streamed long literals are inlined into the plain decode and called by
+// the read kernels, at the compiler's choice (a call there cost registers:
+// 161 -> 168 VGPRs and scratch, round 6).
 #define MHQ_CALLEE __noinline__
-#define MHQ_CALLEE_LONG  // (the compiler's choice: inlined into the plain decode, called by the read kernels)
-#endif
+#define MHQ_CALLEE_LONG
 #ifndef MHQ_DEC_WOUT  // a wave's output slice (bytes, multiple of 16)
 #define MHQ_DEC_WOUT 6448
 #endif
@@ -53,6 +49,7 @@ constexpr int kPF = MHQ_DEC_PF;
 constexpr int kWIn = kPF * kWave * 16;  // input slice bytes (from the tile's 16-B aligned start)
 constexpr int kWOut = MHQ_DEC_WOUT;     // output slice bytes (from the tile's 16-B aligned start)
 constexpr int kBuckets = 64;
+constexpr int kOutRounds = (kWOut + 16 * kWave - 1) / (16 * kWave);  // store_out_batched rounds of a slice
 // wave priority while a wave stages, flushes and sorts a tile (its serial
 // phases), so they do not wait behind the other waves' probe loops (north
 // star 42.8 -> 41.8-42.0 us, round 2)
@@ -690,6 +687,7 @@ __device__ __forceinline__ void decode_piece(const Smem &sm, WaveSmem &ws, uint3
   constexpr int kSteps = kGaps ? MHQ_DEC_STEPS_GAPS : MHQ_DEC_STEPS;
   constexpr bool kPair = MHQ_DEC_PAIR;
   for (uint32_t c = lane; c < (out_bytes + 15u) >> 4; c += kWave) *(u32x4 *)(ws.out_w + 4u * c) = u32x4{0u, 0u, 0u, 0u};
+#ifndef MHQ_X_NOSORT
   // counting sort by encoded length, longest first
   ws.hist[lane] = 0;
   wave_sync();
@@ -717,6 +715,7 @@ __device__ __forceinline__ void decode_piece(const Smem &sm, WaveSmem &ws, uint3
     const uint32_t j = lane + (uint32_t)kWave * h;
     if (j < m) ws.order[ws.hist[key[h]] + rk[h]] = (uint8_t)j;
   }
+#endif
   wave_sync();
   // Lane t decodes rank t, then rank 127 - t if there is one: the 64 longest
   // literals one per lane, the rest on the lanes with the shortest of those
@@ -729,8 +728,13 @@ __device__ __forceinline__ void decode_piece(const Smem &sm, WaveSmem &ws, uint3
 #endif
   const bool hasA = lane < m, hasB = 2u * kWave - 1u - lane < m;
   LitRef<kGaps> A, B;
+#ifdef MHQ_X_NOSORT  // timing build: literals by position (lane t: t and 127 - t), the sort skipped
+  A.load(ws, hasA ? lane : 0u);
+  B.load(ws, hasB ? 2u * kWave - 1u - lane : 0u);
+#else
   A.load(ws, hasA ? ws.order[lane] : 0u);
   B.load(ws, hasB ? ws.order[2u * kWave - 1u - lane] : 0u);
+#endif
   const uint32_t ostartA = A.optr, ostartB = B.optr;
 #ifdef MHQ_DBG_BOUNDS
   {
@@ -1190,7 +1194,7 @@ __device__ MHQ_CALLEE_LONG void decode_tile_long(const SM &sm, W &ws, const uint
     stage_in<true, false>(ws.in_w, kWIn / 4, ia - idelta, in_bytes, lane);
     wave_sync();
     decode_piece<false>(sm, ws, m, out_bytes, lane);
-    store_out(oa - odelta, (const uint8_t *)ws.out_w, odelta, out_bytes, lane);
+    store_out_batched<kOutRounds>(oa - odelta, (const uint8_t *)ws.out_w, odelta, out_bytes, lane);
     flush_lens(ws, s + cur, m, out_len, status, lane);
     wave_sync();
     cur += m;
@@ -1343,7 +1347,7 @@ __device__ __forceinline__ void decode_body(Smem &sm, const uint8_t *__restrict_
     if (pd_o) {
       if (DBG_OK(dbg_out_ok(pd_o + pd_lo, pd_hi - pd_lo), 31, pd_o, pd_hi))
         if (DBG_OK(dbg_out_ok(pd_o + pd_lo, pd_hi - pd_lo), 31, pd_o, pd_hi))
-      store_out(pd_o, (const uint8_t *)ws.out_w, pd_lo, pd_hi, lane);
+      store_out_batched<kOutRounds>(pd_o, (const uint8_t *)ws.out_w, pd_lo, pd_hi, lane);
       flush_lens(ws, pd_s, pd_m, out_len, status, lane, kGaps ? str.kind : nullptr);
     }
     pd_o = nullptr;
@@ -1381,7 +1385,7 @@ __device__ __forceinline__ void decode_body(Smem &sm, const uint8_t *__restrict_
   }
   if (pd_o) {
     if (DBG_OK(dbg_out_ok(pd_o + pd_lo, pd_hi - pd_lo), 31, pd_o, pd_hi))
-      store_out(pd_o, (const uint8_t *)ws.out_w, pd_lo, pd_hi, lane);
+      store_out_batched<kOutRounds>(pd_o, (const uint8_t *)ws.out_w, pd_lo, pd_hi, lane);
     flush_lens(ws, pd_s, pd_m, out_len, status, lane, kGaps ? str.kind : nullptr);
   }
   if (kGaps && str.kind) {

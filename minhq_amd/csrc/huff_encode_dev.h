@@ -22,9 +22,6 @@
 #ifndef MHQ_ENC_OUTCAP  // output staging slice (bytes, encode only)
 #define MHQ_ENC_OUTCAP 20480
 #endif
-#ifndef MHQ_ENC_BRANCHY  // 1: the bit writer ORs a word out under a per-code branch (0, branch free: since r04e, config 2 -1 %, north star -0.7 to -1.3 %)
-#define MHQ_ENC_BRANCHY 0
-#endif
 #ifndef MHQ_ENC_NTST  // encode_len's lengths and the cooperative encode's whole chunks as streaming stores (config 5 encode 162.8 -> 154.9 us)
 #define MHQ_ENC_NTST 1
 #endif
@@ -107,19 +104,13 @@ struct BitOut {
   __device__ __forceinline__ void put(uint32_t code, uint32_t len) {
     acc = (acc << len) | code;
     nbits += len;
-#if MHQ_ENC_BRANCHY
-    if (nbits >= 32u) {
-      nbits -= 32u;
-      atomicOr(&ow[wpos++], __builtin_bswap32((uint32_t)(acc >> nbits)));
-    }
-#else
     // branch free: some lane of the wave completes a word at nearly every
     // byte, so the OR is issued anyway; the others OR 0 into their own word
+    // (a per-code branch: config 2 +1 %, north star +0.7 to 1.3 %, r04e)
     const bool full = nbits >= 32u;
     nbits -= full ? 32u : 0u;
     atomicOr(&ow[wpos], full ? __builtin_bswap32((uint32_t)(acc >> nbits)) : 0u);
     wpos += full ? 1u : 0u;
-#endif
   }
   // Pad with 1 bits to an octet boundary (bitWriter.Pad(0xff)) and OR out the rest.
   __device__ __forceinline__ void finish() {

@@ -230,7 +230,7 @@ __global__ __launch_bounds__(kT) void read_fused_kernel(RsArgs a, const uint32_t
     // before this tile's parse replaces them)
     if (pd_o) {
       if (DBG_OK(dbg_out_ok(pd_o + pd_lo, pd_hi - pd_lo), 34, pd_o, pd_hi))
-        store_out(pd_o, (const uint8_t *)ws.out_w, pd_lo, pd_hi, lane);
+        store_out_batched<kOutRounds>(pd_o, (const uint8_t *)ws.out_w, pd_lo, pd_hi, lane);
       flush_str(ws, pd_s, pd_m, kinds, a.out_len, a.status, lane);
     }
     pd_o = nullptr;
@@ -362,7 +362,7 @@ __global__ __launch_bounds__(kT) void read_fused_kernel(RsArgs a, const uint32_t
   }
   if (pd_o) {
     if (DBG_OK(dbg_out_ok(pd_o + pd_lo, pd_hi - pd_lo), 34, pd_o, pd_hi))
-      store_out(pd_o, (const uint8_t *)ws.out_w, pd_lo, pd_hi, lane);
+      store_out_batched<kOutRounds>(pd_o, (const uint8_t *)ws.out_w, pd_lo, pd_hi, lane);
     flush_str(ws, pd_s, pd_m, kinds, a.out_len, a.status, lane);
   }
 }
