@@ -1346,8 +1346,7 @@ __device__ __forceinline__ void decode_body(Smem &sm, const uint8_t *__restrict_
     // the previous tile's output and lengths leave, then this tile decodes
     if (pd_o) {
       if (DBG_OK(dbg_out_ok(pd_o + pd_lo, pd_hi - pd_lo), 31, pd_o, pd_hi))
-        if (DBG_OK(dbg_out_ok(pd_o + pd_lo, pd_hi - pd_lo), 31, pd_o, pd_hi))
-      store_out_batched<kOutRounds>(pd_o, (const uint8_t *)ws.out_w, pd_lo, pd_hi, lane);
+        store_out_batched<kOutRounds>(pd_o, (const uint8_t *)ws.out_w, pd_lo, pd_hi, lane);
       flush_lens(ws, pd_s, pd_m, out_len, status, lane, kGaps ? str.kind : nullptr);
     }
     pd_o = nullptr;
