@@ -26,10 +26,13 @@
 #ifndef MHQ_DEC_STEPS_GAPS  // the same for the in_end decode of framed strings (read_strings; 3 since r05j: -1..-4 %)
 #define MHQ_DEC_STEPS_GAPS 3
 #endif
-// The decode's out-of-line helper (the checked loop) is a called function;
-// the streamed long literals are inlined into the plain decode and called by
-// the read kernels, at the compiler's choice (a call there cost registers:
-// 161 -> 168 VGPRs and scratch, round 6).
+// The plain decode's out-of-line helper (the checked loop) is a called
+// function; its streamed long literals are inlined at the compiler's choice.
+// The in_end decode (kGaps: read_strings, decode_kernel<true>) inlines both:
+// a call there spilled what was live across it (read_fused_kernel: 11 VGPRs
+// and 74 SGPRs, 48 B of scratch a lane) and reached LDS through generic
+// (flat) pointers; inlined, the read kernels have no call, no flat access
+// and no scratch.
 #define MHQ_CALLEE __noinline__
 #define MHQ_CALLEE_LONG
 #ifndef MHQ_DEC_WOUT  // a wave's output slice (bytes, multiple of 16)
@@ -413,8 +416,8 @@ struct BitBufS {
 // decodes literal bits [p, endbit) into staging bytes [optr, oend) one probe
 // at a time, with the reference's end-of-literal and buffer-full rules
 // (hc/huffman.go:102-121).  Returns out_len | status << 31.
-__device__ MHQ_CALLEE uint32_t decode_checked(const Smem &sm, WaveSmem &ws, uint32_t p, uint32_t endbit,
-                                                uint32_t optr, uint32_t oend) {
+__device__ __forceinline__ uint32_t decode_checked_body(const Smem &sm, WaveSmem &ws, uint32_t p, uint32_t endbit,
+                                                       uint32_t optr, uint32_t oend) {
   BitBuf in;
   in.init(ws.in_w, p);
   OutAcc out;
@@ -449,6 +452,19 @@ __device__ MHQ_CALLEE uint32_t decode_checked(const Smem &sm, WaveSmem &ws, uint
   const uint32_t oend_got = out.optr();
   bad = oend_got != oend ? bad : 0u;
   return (oend_got - ostart) | (bad << 31);
+}
+__device__ MHQ_CALLEE uint32_t decode_checked(const Smem &sm, WaveSmem &ws, uint32_t p, uint32_t endbit,
+                                                uint32_t optr, uint32_t oend) {
+  return decode_checked_body(sm, ws, p, endbit, optr, oend);
+}
+// (kGaps: inlined; see MHQ_CALLEE)
+template <bool kGaps>
+__device__ __forceinline__ uint32_t decode_checked_k(const Smem &sm, WaveSmem &ws, uint32_t p, uint32_t endbit,
+                                                     uint32_t optr, uint32_t oend) {
+  if constexpr (kGaps)
+    return decode_checked_body(sm, ws, p, endbit, optr, oend);
+  else
+    return decode_checked(sm, ws, p, endbit, optr, oend);
 }
 
 // A literal's place in the staged tile.
@@ -836,8 +852,8 @@ __device__ __forceinline__ void decode_piece(const Smem &sm, WaveSmem &ws, uint3
     }
   }
   TL(tls < 0 ? -1 : tls + 1);
-  if (hasA) ws.len[A.lit] = rA != kRedo ? rA : decode_checked(sm, ws, A.p, A.endbit, A.optr, A.oend);
-  if (hasB) ws.len[B.lit] = rB != kRedo ? rB : decode_checked(sm, ws, B.p, B.endbit, B.optr, B.oend);
+  if (hasA) ws.len[A.lit] = rA != kRedo ? rA : decode_checked_k<kGaps>(sm, ws, A.p, A.endbit, A.optr, A.oend);
+  if (hasB) ws.len[B.lit] = rB != kRedo ? rB : decode_checked_k<kGaps>(sm, ws, B.p, B.endbit, B.optr, B.oend);
   wave_sync();
 }
 
@@ -1242,7 +1258,9 @@ __device__ __forceinline__ void decode_body(Smem &sm, const uint8_t *__restrict_
   const uint64_t nb = local ? L1 - L0 : n;
   // read_strings: whether this workgroup finishes its range at the end (its
   // gate word loaded now, used there)
-  const uint64_t fin_gate = kGaps && str.finish_needed ? __builtin_nontemporal_load(str.finish_needed) : 0;
+  // (uniform: a scalar value, not a vector pair live across the tile loop --
+  // read_fallback_kernel spilled that pair to scratch)
+  const uint64_t fin_gate = kGaps && str.finish_needed ? uniform64(__builtin_nontemporal_load(str.finish_needed)) : 0;
   load_off_in<kGaps>(off, in_off, in_end, L0 + (uint64_t)tile * tl0, L1, tl0, lane);
   TileIn tin;
   uint32_t keep[kPF] = {};
@@ -1372,9 +1390,12 @@ __device__ __forceinline__ void decode_body(Smem &sm, const uint8_t *__restrict_
       // (kGaps: every such tile streams)
       if (!kGaps && (ie - ib) <= 2u * (uint64_t)kWIn && (oe - ob) <= 2u * (uint64_t)kWOut)
         decode_tile_pieces(sm, ws, in, in_off, in_bias, out, out_off, out_bias, out_len, status, s, cnt, lane);
+      else if constexpr (kGaps)
+        decode_tile_long_body<kGaps>(sm, ws, in, in_off, in_end, in_bias, out, out_off, out_bias, out_len, status, s,
+                                     cnt, lane, str.kind);
       else
         decode_tile_long<kGaps>(sm, ws, in, in_off, in_end, in_bias, out, out_off, out_bias, out_len, status, s,
-                                cnt, lane, kGaps ? str.kind : nullptr);
+                                cnt, lane);
     }
     TL(tl_slot(tl_j, 5));
     tl_j++;

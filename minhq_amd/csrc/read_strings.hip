@@ -335,8 +335,8 @@ __global__ __launch_bounds__(kT) void read_fused_kernel(RsArgs a, const uint32_t
       }
       __threadfence_block();
       wave_sync();
-      decode_tile_long<true>(sm, ws, a.blk, a.sc_start, a.sc_hend, 0, a.out, a.out_off, 0, a.out_len, a.status, s,
-                             cnt, lane, a.sc_kind);
+      decode_tile_long_body<true>(sm, ws, a.blk, a.sc_start, a.sc_hend, 0, a.out, a.out_off, 0, a.out_len, a.status,
+                                  s, cnt, lane, a.sc_kind);
       __threadfence_block();
       for (uint32_t j = lane; j < cnt; j += kWave) {  // the lane that wrote string j's length
         const uint64_t i = s + j;
