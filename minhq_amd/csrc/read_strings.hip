@@ -323,7 +323,12 @@ __global__ __launch_bounds__(kT) void read_fused_kernel(RsArgs a, const uint32_t
     } else {
       // streamed: out_off[s + cnt] (the last region's end) from the next
       // string's frame, then the long-literal decode over sc_*
-      if (lane == 0 && s + cnt < a.n) {
+      // (every lane parses the same frame -- uniform control flow, scalar
+      // loads -- and lane 0 stores: a lane-0-only block here is where the
+      // register allocator put the copies and spill stores of values live
+      // across the old call, with the other 63 lanes masked off; DESIGN.md,
+      // round 6)
+      if (s + cnt < a.n) {
         const uint64_t i = s + cnt;
         CRUMB(9, a.out_off + i);
         const RsStr r = rs_parse(a.pos[i], min(a.limit[i], blk_len), a.prefix[i], blk_len, 0, blk_len,
@@ -331,7 +336,7 @@ __global__ __launch_bounds__(kT) void read_fused_kernel(RsArgs a, const uint32_t
                                    CRUMB(10, a.blk + q);
                                    return a.blk[q];
                                  });
-        a.out_off[i] = region_at(r.start);
+        if (lane == 0) a.out_off[i] = region_at(r.start);
       }
       __threadfence_block();
       wave_sync();

@@ -265,6 +265,57 @@ def test_read_full_tiles_long_and_raw(codec, oracle_mod):
     assert int((np.asarray(st) == EOF).sum()) == sum(1 for i in range(n) if blk[pos[i]] in (0x80,))
 
 
+def test_read_streamed_then_staged_tiles_every_string(codec, oracle_mod):
+    """Regression for the read path's illegal memory access (DESIGN.md, round
+    6): a wave's streamed tile (a long string: the frames parsed from global
+    memory, lane 0 alone parsing the next tile's first frame, then the
+    streamed decode) followed by staged tiles, many times per wave.  Builds
+    that called the streamed decode out of line had the register allocator
+    copy and spill per-lane values live across the call inside the lane-0
+    block, so lanes 1-63 came back with stale registers (the next tile's
+    positions and limits, the kinds-shuffle lane of strings 64..127).
+    Adjacent strings differ in kind (Huffman OK / empty -> EOF / INVALID,
+    raw, raw empty), so a string handled with another lane's state changes its
+    (value, status); every string and every next is checked."""
+    import numpy as np
+
+    rng = random.Random(61)
+    alpha = b"abcdefghijklmnopqrstuvwxyz0123456789-_./:;=, "
+    palette = [
+        oracle_mod.write_string(b"abc", prefix=7, choice=1),  # Huffman, OK
+        bytes([0x80]),  # Huffman, empty: io.EOF
+        bytes([0x84, 0xFF, 0xFF, 0xFF, 0xFF]),  # Huffman, the EOS code: INVALID
+        bytes([0x03]) + b"xyz",  # raw
+        bytes([0x00]),  # raw, empty
+        oracle_mod.write_string(b"www.example.com/index.html", prefix=7, choice=1),
+    ]
+    expect = [oracle_mod.read_string(f, prefix=7) for f in palette]
+    n = 1 << 17
+    blk, pos, kind, longs = bytearray(), [], [], {}
+    for k in range(n):
+        pos.append(len(blk))
+        if rng.random() < 1 / 300:  # about one tile in three streams
+            s = bytes(rng.choice(alpha) for _ in range(rng.randint(2000, 5000)))
+            f = oracle_mod.write_string(s, prefix=7, choice=1)
+            longs[k] = oracle_mod.read_string(f, prefix=7)
+            kind.append(-1)
+            blk += f
+        else:
+            j = rng.randrange(len(palette))
+            kind.append(j)
+            blk += palette[j]
+    blk = bytes(blk)
+    assert len(longs) > 100
+    vals, st, nxt = codec.read_strings(blk, pos, [7] * n)
+    st, nxt = np.asarray(st), np.asarray(nxt, dtype=np.uint64)
+    bad = []
+    for i in range(n):
+        ref, rc, used = longs[i] if kind[i] < 0 else expect[kind[i]]
+        if (vals[i], int(st[i])) != (ref, _oracle_status(rc)) or int(nxt[i]) != pos[i] + used:
+            bad.append(i)
+    assert not bad, (len(bad), bad[:10])
+
+
 @pytest.mark.parametrize("order", ["block", "shuffled", "overlap"])
 def test_read_random_bytes_as_frames(codec, oracle_mod, order):
     """Random octets read as frames at increasing positions: each string's
