@@ -25,8 +25,17 @@
 // per caller stream for look-backs only (mhq_api.cpp), so a slot holds this
 // call's tag or an earlier call's, never another entry point's data; a
 // workgroup only waits for lower-numbered ones, which the dispatcher started
-// first, so the grid need not be resident at once.
+// first, so the grid need not be resident at once.  First is per XCD,
+// though: the dispatcher starts a launch's workgroups in order on each XCD,
+// not across the chip, so with concurrent launches (several streams) a
+// workgroup can be resident and polling while a predecessor waits for a
+// slot on another XCD that other polling workgroups hold.  A predecessor
+// still unpublished after MHQ_PK_HELP_POLLS polls is therefore sized by the
+// polling workgroup itself from global memory: the look-back
+// never depends on a workgroup being scheduled.
 #include <hip/hip_runtime.h>
+
+#include <cstdlib>
 
 #include "huff_encode_dev.h"
 
@@ -79,6 +88,11 @@ __device__ unsigned long long g_pktl[kPkWgs * kPkSlots];
 #ifndef MHQ_PK_FOUR_RANGE_BYTES  // the four-workgroup shape up to this mean range of kT literals (bytes)
 #define MHQ_PK_FOUR_RANGE_BYTES 19200
 #endif
+#ifndef MHQ_PK_LBW  // look-back windows of 64 predecessors read per round trip (r06: 3, 4 costs more with the stuck exit)
+#define MHQ_PK_LBW 3
+#endif
+constexpr int kLbW = MHQ_PK_LBW;
+
 template <int kB>
 struct PkShape {
   static constexpr int kIn = kB >= 4 ? 20224 : kInCap;    // plaintext staging (bytes)
@@ -101,6 +115,7 @@ struct alignas(16) PackSmem {
   uint32_t rel[kT];                 // by literal: enc_len, then its range-relative output offset
   uint32_t wsum[2][kT / kWave];     // per-wave totals of enc_len and capacity
   uint64_t base[2];                 // the range's place: enc and capacity bytes before it
+  uint64_t stuck;                   // a predecessor range look_back found unpublished too long, or ~0
   static_assert(kPkIn + 16 < 65536, "rec holds 16-bit input indices");
   static_assert(sizeof(uint16_t) * kT + sizeof(uint32_t) * kBuckets <= sizeof(uint32_t) * (kPkOut / 4 + 4),
                 "sort in staging");
@@ -118,6 +133,7 @@ struct PackArgs {
   uint32_t tag;     // the call's look-back tag: 30 bits, never 0
   uint32_t R;       // literals per range: kT, or kShortR (launch_encode_packed)
   uint64_t in_bytes;  // the caller's in_off[n] - in_off[0], verified by every workgroup
+  uint32_t help_polls;  // polls of a predecessor's slot before the polling wave sizes its range itself
 };
 
 // A look-back slot: [63:34] the call's tag, [33:32] 1 aggregate / 2
@@ -134,10 +150,6 @@ __device__ __forceinline__ uint64_t wave_sum64(uint64_t v) {
   return v;
 }
 
-#ifndef MHQ_PK_LBW  // look-back windows of 64 predecessors read per round trip
-#define MHQ_PK_LBW 4
-#endif
-constexpr int kLbW = MHQ_PK_LBW;
 
 // Totals (enc, cap) of workgroups [0, b), by ONE wave: lane l reads the
 // slots of workgroups b - 1 - l - 64 k (k < kLbW windows at once, spinning
@@ -147,10 +159,13 @@ constexpr int kLbW = MHQ_PK_LBW;
 // next kLbW windows are read.  (One wave per workgroup polls, no workgroup
 // barrier; in a generation of ranges started together the nearest inclusive
 // prefix can lie several windows back.)
-__device__ void look_back(const PackArgs &a, uint32_t b, uint32_t lane, uint64_t &se, uint64_t &sc) {
+// Returns false, with `stuck` one of them, when a predecessor's slots stay
+// unpublished past a.help_polls polls (see the top).
+__device__ bool look_back(const PackArgs &a, uint32_t b, uint32_t lane, uint64_t &se, uint64_t &sc,
+                          uint64_t &stuck) {
   se = sc = 0;
   bool de = false, dc = false;  // (uniform over the wave)
-  const unsigned long long *sl = (const unsigned long long *)a.slots;
+  unsigned long long *sl = (unsigned long long *)a.slots;
   for (int64_t hi = (int64_t)b - 1; hi >= 0 && !(de && dc); hi -= (int64_t)kWave * kLbW) {
     uint64_t ve[kLbW], vc[kLbW];
 #pragma unroll
@@ -165,10 +180,19 @@ __device__ void look_back(const PackArgs &a, uint32_t b, uint32_t lane, uint64_t
 #pragma unroll
     for (int k = 0; k < kLbW; k++) {
       const int64_t g = hi - (int64_t)kWave * k - (int64_t)lane;
-      while (g >= 0 && ((uint32_t)(ve[k] >> 34) != a.tag || (uint32_t)(vc[k] >> 34) != a.tag)) {
+      // polled as a wave (the poll count is scalar)
+      uint32_t polls = 0;
+      for (uint64_t m; (m = __ballot(g >= 0 && ((uint32_t)(ve[k] >> 34) != a.tag ||
+                                                 (uint32_t)(vc[k] >> 34) != a.tag))) != 0;) {
+        if (++polls > a.help_polls) {
+          stuck = (uint64_t)(hi - (int64_t)kWave * k - (int64_t)__builtin_ctzll(m));
+          return false;
+        }
         if (MHQ_PK_SLEEP) __builtin_amdgcn_s_sleep(MHQ_PK_SLEEP);
-        ve[k] = __hip_atomic_load(sl + 2 * g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        vc[k] = __hip_atomic_load(sl + 2 * g + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (g >= 0 && ((uint32_t)(ve[k] >> 34) != a.tag || (uint32_t)(vc[k] >> 34) != a.tag)) {
+          ve[k] = __hip_atomic_load(sl + 2 * g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          vc[k] = __hip_atomic_load(sl + 2 * g + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
       }
     }
 #pragma unroll
@@ -188,6 +212,7 @@ __device__ void look_back(const PackArgs &a, uint32_t b, uint32_t lane, uint64_t
       dc = dc || stop_c < (uint32_t)kWave;
     }
   }
+  return true;
 }
 
 // Global bytes [lo, hi) from o_al (16-B aligned) <- staging bytes
@@ -357,21 +382,60 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu((kT / 64 * k
     }
   }
   // the predecessors' totals (one wave), then this range's inclusive prefix
-  if (wave == 0) {
-    PKTL(b, 5, lane == 0);
-    uint64_t se, sc;
-    look_back(a, b, lane, se, sc);
-    PKTL(b, 6, lane == 0);
-    if (lane == 0) {
-      sm.base[0] = se;
-      sm.base[1] = sc;
-      __hip_atomic_store((unsigned long long *)a.slots + 2 * b, pack_slot(a.tag, 2u, (uint32_t)(se + T)),
-                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store((unsigned long long *)a.slots + 2 * b + 1, pack_slot(a.tag, 2u, (uint32_t)(sc + C)),
-                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  for (;;) {
+    if (wave == 0) {
+      PKTL(b, 5, lane == 0);
+      uint64_t se, sc, stuck = 0;
+      const bool done = look_back(a, b, lane, se, sc, stuck);
+      PKTL(b, 6, lane == 0);
+      if (lane == 0) {
+        sm.stuck = done ? ~0ull : stuck;
+        if (done) {
+          sm.base[0] = se;
+          sm.base[1] = sc;
+          __hip_atomic_store((unsigned long long *)a.slots + 2 * b, pack_slot(a.tag, 2u, (uint32_t)(se + T)),
+                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store((unsigned long long *)a.slots + 2 * b + 1, pack_slot(a.tag, 2u, (uint32_t)(sc + C)),
+                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+      }
     }
+    __syncthreads();  // the base; the staging complete
+    const uint64_t g = uniform64(sm.stuck);
+    if (g == ~0ull) break;
+    // range g stayed unpublished (see the top): this workgroup sizes it, a
+    // literal a thread, publishes its aggregate on its behalf -- the value
+    // its own workgroup publishes too -- and looks back again
+    const uint64_t Lg = g * a.R;
+    const uint32_t cg = (uint32_t)min((uint64_t)a.R, n - Lg);
+    uint32_t hv = 0;
+    if (tid < cg) {  // (a plain byte loop: a rare path, kept small)
+      uint32_t bits = 0;
+      const uint8_t *q = a.in + (a.in_off[Lg + tid] - a.in_bias), *qe = a.in + (a.in_off[Lg + tid + 1] - a.in_bias);
+      for (; q < qe; q++) bits += sm.code[*q].y;
+      hv = (bits + 7u) >> 3;
+    }
+    const uint64_t hw = wave_sum64((uint64_t)hv | (uint64_t)((uint64_t)hv * 8u / 5u) << 32);
+    if (lane == 0) {
+      sm.wsum[0][wave] = (uint32_t)hw;
+      sm.wsum[1][wave] = (uint32_t)(hw >> 32);
+    }
+    __syncthreads();
+    if (tid == 0) {
+      uint32_t te = 0, tc = 0;
+#pragma unroll
+      for (int w = 0; w < kT / kWave; w++) {
+        te += sm.wsum[0][w];
+        tc += sm.wsum[1][w];
+      }
+      __hip_atomic_store((unsigned long long *)a.slots + 2 * g, pack_slot(a.tag, 1u, te), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store((unsigned long long *)a.slots + 2 * g + 1, pack_slot(a.tag, 1u, tc), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+      __threadfence();
+    }
+    __syncthreads();
   }
-  __syncthreads();  // the base; the staging complete
   PKTL(b, 7, tid == 0);
   const uint64_t base_e = sm.base[0], base_c = sm.base[1];
   if (tid < cnt) {
@@ -397,7 +461,8 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu((kT / 64 * k
     store_out_shifted(oa - odelta, sm.out_w, odelta, odelta + (uint32_t)min((uint64_t)T, room), odelta, tid, kT);
   } else if (tid < cnt && v && rel_e + v <= room) {
     const uint64_t s0 = a.in_off[L0 + tid];
-    encode_literal_global<true>(a.in + (s0 - a.in_bias), e_t - s0, oa + rel_e, sm.code, nullptr);
+    const uint64_t e0 = a.in_off[L0 + tid + 1];  // (loaded again: e_t is not kept live across the look-back)
+    encode_literal_global<true>(a.in + (s0 - a.in_bias), e0 - s0, oa + rel_e, sm.code, nullptr);
   }
   PKTL(b, 8, tid == 0);
 }
@@ -429,6 +494,20 @@ static_assert(kShortR <= (uint32_t)kT && kShortR % kWave == 0, "range size");
 // (for either range size)
 size_t encode_packed_slot_bytes(uint64_t n) { return 16u * ((n + kShortR - 1) / kShortR); }
 
+#ifndef MHQ_PK_HELP_POLLS  // ~100 us of polls (a generation of ranges publishes within ~20 us)
+#define MHQ_PK_HELP_POLLS 400
+#endif
+// The look-backs' patience (the packed encode's, read_fallback_kernel's):
+// MHQ_PK_HELP_POLLS, or the environment's, read once (tests force the help
+// with 0).
+uint32_t lookback_help_polls() {
+  static const uint32_t t = [] {
+    const char *e = getenv("MHQ_PK_HELP_POLLS");
+    return e ? (uint32_t)strtoul(e, nullptr, 10) : (uint32_t)MHQ_PK_HELP_POLLS;
+  }();
+  return t;
+}
+
 hipError_t launch_encode_packed(const DevTables &t, const uint8_t *in, const uint64_t *in_off, uint64_t in_bias,
                                 uint64_t n, uint64_t base, uint32_t *enc_len, uint64_t *out_off, uint64_t *cap_off,
                                 uint8_t *out, uint64_t out_cap, uint64_t *slots, uint32_t tag, hipStream_t s,
@@ -443,8 +522,8 @@ hipError_t launch_encode_packed(const DevTables &t, const uint8_t *in, const uin
   const bool four = in_bytes * (uint64_t)kShortR <= fit;
   const uint32_t R = four && in_bytes * (uint64_t)kT > fit ? kShortR : (uint32_t)kT;
   const unsigned grid = (unsigned)((n + R - 1) / R);
-  PackArgs a{in, in_off, in_bias, n, base, enc_len, out_off, cap_off, out, out_cap, slots, (uint32_t)tag, R,
-             in_bytes};
+  PackArgs a{in,   in_off, in_bias, n, base, enc_len, out_off, cap_off, out, out_cap, slots, (uint32_t)tag, R,
+             in_bytes, lookback_help_polls()};
   if (four)
     encode_packed_kernel<4><<<dim3(grid), dim3(kT), 0, s>>>(a, t.code, t.len);
   else

@@ -911,7 +911,11 @@ struct OutAccG {
   __device__ __forceinline__ void flush(uint32_t *gout) {
     const bool full = ab >= 32u;
     const uint32_t v = (uint32_t)acc;
+#ifdef MHQ_X_LONG_NOSTORE  // timing build: the streamed path's word stores skipped (wrong output)
+    if (false) {
+#else
     if (full && ow >= owf) {
+#endif
       CRUMB(53, gout + ow);
       if (!grouped(ow)) {
         if (DBG_OK(dbg_out_ok(gout + ow, 4), 23, gout + ow, ow)) gout[ow] = v;

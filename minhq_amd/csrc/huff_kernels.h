@@ -44,6 +44,9 @@ hipError_t launch_encode(const DevTables &t, const uint8_t *in, const uint64_t *
 // in_bytes must be in_off[n] - in_off[0]: otherwise nothing is encoded and
 // out_off[n] = UINT64_MAX.
 size_t encode_packed_slot_bytes(uint64_t n);
+// Polls of an unpublished predecessor before a look-back computes its sum
+// itself (enc_packed.hip, read_strings.hip's fallback).
+uint32_t lookback_help_polls();
 hipError_t launch_encode_packed(const DevTables &t, const uint8_t *in, const uint64_t *in_off, uint64_t in_bias,
                                 uint64_t n, uint64_t base, uint32_t *enc_len, uint64_t *out_off, uint64_t *cap_off,
                                 uint8_t *out, uint64_t out_cap, uint64_t *slots, uint32_t tag, hipStream_t s,

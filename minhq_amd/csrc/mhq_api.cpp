@@ -247,6 +247,7 @@ void *stream_buffer(Device *d, std::vector<Device::Scratch> &pool, hipStream_t s
     x.p = p;
     x.bytes = b;
     x.holders = 1;
+    x.tag = 0;  // (the slots pool: a new buffer is zeroed before its first call)
     return x.p;
   }
   if (pool.size() >= kMaxScratchStreams) return nullptr;
@@ -262,9 +263,10 @@ void *stream_scratch(Device *d, hipStream_t s, size_t bytes) { return stream_buf
 // The packed encode's look-back slots for one call on stream s, and the
 // call's tag (1 .. 2^30 - 1).  A slot whose tag equals the call's is taken
 // as this call's, so the tags are per buffer and stream-ordered: a new
-// buffer is zeroed (tag 0 is never handed out), and when a buffer's tags
-// wrap it is zeroed again in stream order before the call that restarts at 1
-// (stale slots of an older, larger call).
+// buffer is zeroed (tag 0 is never handed out; a buffer replaced to grow
+// starts over at 0 too), and when a buffer's tags wrap it is zeroed again in
+// stream order before the call that restarts at 1 (ADVICE r5:
+// stale slots of an older, larger call).
 constexpr uint32_t kMaxSlotTag = (1u << 30) - 1u;
 void *take_slots(Device *d, hipStream_t s, size_t bytes, uint32_t *tag) {
   void *p = stream_buffer(d, d->slots, s, bytes);

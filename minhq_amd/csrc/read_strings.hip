@@ -394,12 +394,29 @@ struct RsFallback {
   uint64_t out_cap;
   uint64_t *wg_agg;  // per workgroup: agg_tag(gen) | capacity sum (0 until published; cleared by the fused pass)
   uint64_t *wg_fin;  // per workgroup: gen when its range holds a raw string
+  uint32_t help_polls;  // polls of a predecessor's sum before it is computed here (see the look-back)
 };
 constexpr uint64_t kAggBits = 40;  // a workgroup's capacity sum < 2^40
 // A published sum's tag: 23 bits of the call's generation number and a set
 // bit, never 0, so a cleared slot never matches (and the read_fused_kernel
 // clears every slot before this launch).
 __device__ __forceinline__ uint64_t agg_tag(uint64_t gen) { return ((gen & 0x7fffffull) | 0x800000ull) << kAggBits; }
+
+// The capacity sum workgroup g publishes (its strings [L0, L1)), computed
+// by one thread from the frames in global memory: the look-back's way out
+// when g stays unpublished -- the dispatcher starts workgroups in order per
+// XCD, not across the chip, so with concurrent launches g may be waiting for
+// a slot that polling workgroups hold.
+__device__ __forceinline__ uint64_t range_cap_sum(const RsArgs &a, uint64_t L0, uint64_t L1) {
+  uint64_t csum = 0;
+  for (uint64_t i = L0; i < L1; i++) {
+    const RsStr r = rs_parse(a.pos[i], min(a.limit[i], a.blk_len), a.prefix[i], a.blk_len, 0, a.blk_len,
+                             [&](uint64_t q) -> uint32_t { return a.blk[q]; });
+    const uint32_t k = r.kind & 3u;
+    csum += k == 1u ? r.take * 8u / 5u : (k == 0u ? r.take : 0u);
+  }
+  return csum;
+}
 
 // Sum of v over the workgroup (every thread gets it); red: kWaves words.
 __device__ __forceinline__ uint64_t wg_sum(uint64_t v, uint64_t *red) {
@@ -459,9 +476,13 @@ __global__ __launch_bounds__(kT) void read_fallback_kernel(RsFallback f, const u
     const uint32_t g = g0 + tid;
     uint64_t v = 0;
     if (g < b) {
-      for (;;) {
+      for (uint32_t polls = 0;; polls++) {
         v = __hip_atomic_load((unsigned long long *)f.wg_agg + g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if ((v & ~((1ull << kAggBits) - 1u)) == tag) break;
+        if (polls >= f.help_polls) {  // unpublished too long: its sum from its frames (range_cap_sum)
+          v = tag | range_cap_sum(a, (uint64_t)g * per_block, min((uint64_t)g * per_block + per_block, n));
+          break;
+        }
         __builtin_amdgcn_s_sleep(1);
       }
     }
@@ -584,7 +605,7 @@ hipError_t launch_read_fallback(const DevTables &t, const uint8_t *blk, uint64_t
   if (grid > kReadFallbackMaxWgs) return hipErrorInvalidConfiguration;
   RsFallback f{RsArgs{blk, blk_len, pos, limit, prefix, n, out, out_off, next, out_len, status, sc_start, sc_hend,
                       sc_kind, fallback, gen, wg_agg},
-               out_cap, wg_agg, wg_fin};
+               out_cap, wg_agg, wg_fin, lookback_help_polls()};
   MHQ_DBG_SET_MEM(out, out + out_cap, blk, blk + ((blk_len + 15) & ~(uint64_t)15));
   read_fallback_kernel<<<dim3(grid), dim3(kT), 0, s>>>(f, t.lut1, t.lut2, t.len, per_block, (uint32_t)tl);
   return hipGetLastError();

@@ -174,6 +174,40 @@ def test_packed_repeated_calls_two_streams(codec, oracle_mod):
         _run(codec, oracle_mod, b.data, b.off, stream=None if k % 2 == 0 else s2.cuda_stream)
 
 
+def test_packed_concurrent_launches_four_streams(codec, oracle_mod):
+    """Twelve 2^18-literal encodes in flight at once over four streams, no
+    synchronisation between them: concurrent launches share the CUs, and a
+    range is claimed by ticket (enc_packed.hip), so a workgroup never waits on
+    a range no running workgroup holds.  Every call against the oracle."""
+    import torch
+
+    from minhq_amd import workloads as w
+
+    dev = torch.device("cuda:0")
+    streams = [torch.cuda.Stream().cuda_stream for _ in range(4)]
+    b = w.north_star(1 << 18)
+    n, in_bytes = b.n, int(b.off[-1])
+    t_data = torch.from_numpy(b.data.copy()).to(dev)
+    t_off = torch.from_numpy(b.off.view(np.int64).copy()).to(dev)
+    cap = 30 * in_bytes // 8 + n
+    calls = [(torch.full((n,), -1, dtype=torch.int32, device=dev), torch.full((n + 1,), -1, dtype=torch.int64,
+                                                                              device=dev),
+              torch.full((cap,), 0xA5, dtype=torch.uint8, device=dev)) for _ in range(12)]
+    torch.cuda.synchronize()
+    for k, (enc_len, out_off, out) in enumerate(calls):
+        codec.encode_packed_dev(t_data, t_off, in_bytes, enc_len, out_off, None, out, base=k,
+                                stream=streams[k % 4])
+    torch.cuda.synchronize()
+    ref_len = oracle_mod.encode_len_batch(b.data, b.off, nthreads=8)
+    eoff = np.zeros(n + 1, dtype=np.uint64)
+    eoff[1:] = np.cumsum(ref_len, dtype=np.uint64)
+    ref_enc = oracle_mod.encode_batch(b.data, b.off, eoff, nthreads=8).tobytes()
+    for k, (enc_len, out_off, out) in enumerate(calls):
+        assert np.array_equal(enc_len.cpu().numpy().view(np.uint32), ref_len), k
+        assert np.array_equal(out_off.cpu().numpy().view(np.uint64), eoff + k), k
+        assert out.cpu().numpy()[: int(eoff[-1])].tobytes() == ref_enc, k
+
+
 def test_packed_rejects_small_out(codec):
     import torch
 

@@ -93,7 +93,7 @@ def main():
             per = b.nbytes + enc_bytes + 16 * n
             alg = b.nbytes + enc_bytes + 16 * (n + 1) + 4 * n
         elif args.kernel in ("packed", "layenc"):  # the encode side: plaintext in, lengths, offsets, codes out
-            per = b.nbytes + (30 * b.nbytes + 7) // 8 + 32 * n
+            per = b.nbytes + 30 * b.nbytes // 8 + 33 * n
             alg = b.nbytes + enc_bytes + 8 * (n + 1) + 4 * n + 8 * (n + 1) + 8 * (n + 1)
         else:
             per = b.nbytes + 32 * n
@@ -110,7 +110,7 @@ def main():
             else:
                 s["in"], s["off"] = data.clone(), off.clone()
                 s["eoff"] = enc_off.clone()
-                s["out"] = torch.empty(max(enc_bytes + 16, (30 * b.nbytes + 7) // 8), dtype=torch.uint8, device=dev)
+                s["out"] = torch.empty(max(enc_bytes + 16, 30 * b.nbytes // 8 + n), dtype=torch.uint8, device=dev)
                 s["len"] = torch.empty(n, dtype=torch.int32, device=dev)
                 s["o1"] = torch.empty_like(enc_off)
                 s["o2"] = torch.empty_like(cap_off)
