@@ -172,6 +172,12 @@ int mhq_huff_decode_sized_dev(mhq_ctx *ctx, int dev, const uint8_t *in, const ui
 #define MHQ_DECODE_STREAM 2
 int mhq_set_decode_form(int form);
 
+/* Test hook (no reference counterpart): while set, every read_strings call
+ * first fills its fallback word and look-back slots with stale values that
+ * match the call in round 4's compare forms (tests/test_strings.py::
+ * test_read_poisoned_scratch).  Process-wide; returns the previous setting. */
+int mhq_debug_poison_scratch(int on);
+
 /* ---------------- string literals: H bit + prefix integer + payload --------
  * Batch Reader.ReadString(prefix) and Writer.WriteStringRaw(s, prefix, choice)
  * (hc/io.go:73-97, 153-197) with the prefix integers of Reader.ReadInt /

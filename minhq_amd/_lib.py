@@ -64,6 +64,7 @@ SIGNATURES = {
     "mhq_huff_decode_dev": (C.c_int, [vp, C.c_int, vp, vp, C.c_uint64, vp, vp, vp, vp, vp]),
     "mhq_huff_decode_sized_dev": (C.c_int, [vp, C.c_int, vp, vp, C.c_uint64, C.c_uint64, vp, vp, vp, vp, vp]),
     "mhq_set_decode_form": (C.c_int, [C.c_int]),
+    "mhq_debug_poison_scratch": (C.c_int, [C.c_int]),
     "mhq_read_strings_dev": (C.c_int, [vp, C.c_int, vp, C.c_uint64, vp, vp, vp, C.c_uint64, vp, C.c_uint64,
                                        vp, vp, vp, vp, vp]),
     "mhq_write_strings_dev": (C.c_int, [vp, C.c_int, vp, vp, C.c_uint64, vp, vp, C.c_int, vp, C.c_uint64,

@@ -2,6 +2,8 @@
 // Internal to libmhq_huff.so; the public surface is include/mhq_huff.h.
 #pragma once
 #include <hip/hip_runtime.h>
+
+#include <atomic>
 #include <stdint.h>
 
 #include "../../include/mhq_huff.h"
@@ -91,6 +93,9 @@ hipError_t launch_decode_stream(const DevTables &t, const uint8_t *in, const uin
 enum DecodeForm { kDecodeAuto = 0, kDecodeTile = 1, kDecodeStream = 2 };
 int decode_form();
 int set_decode_form(int form);  // the previous form, -1 for an unknown one
+// Test hook (mhq_debug_poison_scratch): read_strings poisons its fallback
+// word and look-back slots with round 4's matching forms before each call.
+extern std::atomic<int> debug_poison_scratch;
 // in_bytes (the batch's encoded bytes, 0 if unknown): a mean literal over
 // kLongMean bytes takes the long-literal form (decode_long_kernel)
 #ifndef MHQ_DEC_LONG_MEAN

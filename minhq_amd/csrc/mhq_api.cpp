@@ -738,6 +738,8 @@ int mhq_set_decode_form(int form) {
   return prev < 0 ? MHQ_EINVAL : prev;
 }
 
+int mhq_debug_poison_scratch(int on) { return mhq::debug_poison_scratch.exchange(on ? 1 : 0); }
+
 int mhq_huff_decode_dev(mhq_ctx *ctx, int dev, const uint8_t *in, const uint64_t *in_off, uint64_t n,
                         uint8_t *out, const uint64_t *out_off, uint32_t *out_len, uint8_t *status,
                         void *stream) {

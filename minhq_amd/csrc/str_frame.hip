@@ -476,6 +476,8 @@ size_t read_strings_scratch_bytes(uint64_t n, uint64_t blk_len) { return ReadLay
 // unless parse stored this call's generation number to order_bad (a number
 // no earlier call used: no reset, and stale scratch contents can only cause
 // the always-correct scan).
+std::atomic<int> debug_poison_scratch{0};  // mhq_debug_poison_scratch (test hook)
+
 hipError_t launch_read_strings(const DevTables &t, const uint8_t *blk, uint64_t blk_len, const uint64_t *pos,
                                const uint64_t *limit, const uint8_t *prefix, uint64_t n, uint8_t *out,
                                uint64_t out_cap, uint64_t *out_off, uint32_t *out_len, uint8_t *status,
@@ -502,7 +504,7 @@ hipError_t launch_read_strings(const DevTables &t, const uint8_t *blk, uint64_t 
   // launch that returns at once unless the pass stored gen to *fallback
   if (kFused) {
     uint64_t *coop = (uint64_t *)(base + L.coop);
-    if (getenv("MHQ_DEBUG_POISON_SCRATCH")) {
+    if (debug_poison_scratch.load(std::memory_order_relaxed)) {
       read_poison_kernel<<<(kReadFallbackMaxWgs + 255) / 256, 256, 0, s>>>(fallback, coop, gen);
       TRY(hipGetLastError());
     }

@@ -452,7 +452,7 @@ def test_read_regions_layout(codec, oracle_mod, order):
 @pytest.mark.parametrize("order", ["in_order", "runs"])
 def test_read_poisoned_scratch(codec, oracle_mod, monkeypatch, order):
     """Stale scratch that matches the call's flags in their round-4 form
-    (MHQ_DEBUG_POISON_SCRATCH, str_frame.hip): a fallback word whose LOW word
+    (mhq_debug_poison_scratch, str_frame.hip): a fallback word whose LOW word
     equals the call's generation number -- round 4's fused pass compared only
     that and stopped its waves, while the fallback, comparing all 64 bits, did
     nothing: strings left unwritten -- and look-back slots carrying round 4's
@@ -491,10 +491,12 @@ def test_read_poisoned_scratch(codec, oracle_mod, monkeypatch, order):
     out_len = torch.full((n,), -1, dtype=torch.int32, device=dev)
     st = torch.full((n,), 0xEE, dtype=torch.uint8, device=dev)
     nxt = torch.full((n,), -1, dtype=torch.int64, device=dev)
-    monkeypatch.setenv("MHQ_DEBUG_POISON_SCRATCH", "1")
-    codec.read_strings_dev(t_blk, t_pos, t_lim, t_pf, out, out_off, out_len, st, nxt)
-    torch.cuda.synchronize()
-    monkeypatch.delenv("MHQ_DEBUG_POISON_SCRATCH")
+    codec._L.mhq_debug_poison_scratch(1)
+    try:
+        codec.read_strings_dev(t_blk, t_pos, t_lim, t_pf, out, out_off, out_len, st, nxt)
+        torch.cuda.synchronize()
+    finally:
+        codec._L.mhq_debug_poison_scratch(0)
     oo = out_off.cpu().numpy().view(np.uint64)
     ol = out_len.cpu().numpy().view(np.uint32)
     assert (st.cpu().numpy() == np.asarray(ref_st)).all()

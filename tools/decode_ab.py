@@ -57,6 +57,7 @@ def main():
     ap.add_argument("--rotate-gib", type=float, default=1.0)
     ap.add_argument("--n", type=int, default=0)
     ap.add_argument("--diag", action="store_true", help="a -DMHQ_DIAG_STREAM build (MHQ_LIB_PATH): per-wave counters")
+    ap.add_argument("--sized", action="store_true", help="decode through mhq_huff_decode_sized_dev (the long-literal form for long batches)")
     args = ap.parse_args()
 
     import torch
@@ -80,7 +81,8 @@ def main():
 
             def run(i):
                 s = slots[i % len(slots)]
-                codec.decode_dev(s.enc, s.enc_off, s.out, s.cap_off, s.out_len, s.status)
+                codec.decode_dev(s.enc, s.enc_off, s.out, s.cap_off, s.out_len, s.status,
+                                 in_bytes=dv.enc_bytes if args.sized else 0)
 
             for s in slots[:2]:
                 s.out.zero_()

@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--long", type=int, default=2000)
     ap.add_argument("--streams", default="4", help="comma-separated stream counts to try")
+    ap.add_argument("--chain", default="0", help="comma-separated: 1 = each step's encode waits for the previous step's encode (an event)")
     args = ap.parse_args()
 
     import torch
@@ -44,14 +45,35 @@ def main():
         bench.round_trip(codec, s)
         bench.verify_slot(s)
     all_streams = [torch.cuda.Stream(device=dev).cuda_stream for _ in range(4)]
-    for S in [int(x) for x in args.streams.split(",")]:
-        streams = all_streams[:S]
-        bound = [bench.bind_round_trip(codec, slots[i], streams[i % S]) for i in range(R)]
-        probe(args, torch, bench, codec, slots, streams, bound, R, S)
+    import ctypes as C
+
+    hip = C.CDLL("libamdhip64.so")
+    hip.hipEventCreateWithFlags.argtypes = [C.POINTER(C.c_void_p), C.c_uint]
+    hip.hipEventRecord.argtypes = [C.c_void_p, C.c_void_p]
+    hip.hipStreamWaitEvent.argtypes = [C.c_void_p, C.c_void_p, C.c_uint]
+    evs = [C.c_void_p() for _ in range(4)]
+    for e in evs:
+        assert hip.hipEventCreateWithFlags(C.byref(e), 2) == 0
+    for chain in [int(x) for x in args.chain.split(",")]:
+        for S in [int(x) for x in args.streams.split(",")]:
+            streams = all_streams[:S]
+            bound = [bench.bind_round_trip(codec, slots[i], streams[i % S]) for i in range(R)]
+            if chain:
+                bound = [chained(hip, evs, bound[i], streams[i % S], i) for i in range(R)]
+            probe(args, torch, bench, codec, slots, streams, bound, R, S, chain)
     codec.close()
 
 
-def probe(args, torch, bench, codec, slots, streams, bound, R, S):
+def chained(hip, evs, calls, stream, i):
+    """Step i's calls with its encode after step i - 1's (stream i % S waits
+    for the event recorded after the previous step's encode)."""
+    enc, dec = calls
+    wait_ev, rec_ev = evs[(i - 1) % len(evs)], evs[i % len(evs)]
+    # (R is a multiple of len(evs): slot i's events are the same on every pass)
+    return (lambda: hip.hipStreamWaitEvent(stream, wait_ev, 0), enc, lambda: hip.hipEventRecord(rec_ev, stream), dec)
+
+
+def probe(args, torch, bench, codec, slots, streams, bound, R, S, chain=0):
 
     def run(k, warm=5):
         for i in range(warm):
@@ -72,7 +94,7 @@ def probe(args, torch, bench, codec, slots, streams, bound, R, S):
     sub = np.array([o[0] for o in out])
     tot = np.array([o[1] for o in out])
     _, tot_long = run(args.long)
-    res = {"streams": S, "steps": args.steps, "submit_us_med": round(float(np.median(sub)), 1),
+    res = {"streams": S, "chain": chain, "steps": args.steps, "submit_us_med": round(float(np.median(sub)), 1),
            "submit_us_per_step": round(float(np.median(sub)) / args.steps, 2),
            "total_us_med": round(float(np.median(tot)), 1),
            "us_per_step_med": round(float(np.median(tot)) / args.steps, 2),
