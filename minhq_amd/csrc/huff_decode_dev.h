@@ -703,7 +703,6 @@ __device__ __forceinline__ void decode_piece(const Smem &sm, WaveSmem &ws, uint3
   constexpr int kSteps = kGaps ? MHQ_DEC_STEPS_GAPS : MHQ_DEC_STEPS;
   constexpr bool kPair = MHQ_DEC_PAIR;
   for (uint32_t c = lane; c < (out_bytes + 15u) >> 4; c += kWave) *(u32x4 *)(ws.out_w + 4u * c) = u32x4{0u, 0u, 0u, 0u};
-#ifndef MHQ_X_NOSORT
   // counting sort by encoded length, longest first
   ws.hist[lane] = 0;
   wave_sync();
@@ -731,26 +730,15 @@ __device__ __forceinline__ void decode_piece(const Smem &sm, WaveSmem &ws, uint3
     const uint32_t j = lane + (uint32_t)kWave * h;
     if (j < m) ws.order[ws.hist[key[h]] + rk[h]] = (uint8_t)j;
   }
-#endif
   wave_sync();
   // Lane t decodes rank t, then rank 127 - t if there is one: the 64 longest
   // literals one per lane, the rest on the lanes with the shortest of those
   // (LPT).  The lane's two fast loops run back to back in one loop (it moves
   // to its second literal in place), so lanes stay busy until all are done.
-#ifdef MHQ_X_NODEC  // timing build only (wrong output): staging, sort, zeroing and stores, no decoding
-  if (lane < m) ws.len[lane] = 0;
-  wave_sync();
-  return;
-#endif
   const bool hasA = lane < m, hasB = 2u * kWave - 1u - lane < m;
   LitRef<kGaps> A, B;
-#ifdef MHQ_X_NOSORT  // timing build: literals by position (lane t: t and 127 - t), the sort skipped
-  A.load(ws, hasA ? lane : 0u);
-  B.load(ws, hasB ? 2u * kWave - 1u - lane : 0u);
-#else
   A.load(ws, hasA ? ws.order[lane] : 0u);
   B.load(ws, hasB ? ws.order[2u * kWave - 1u - lane] : 0u);
-#endif
   const uint32_t ostartA = A.optr, ostartB = B.optr;
 #ifdef MHQ_DBG_BOUNDS
   {
@@ -911,11 +899,7 @@ struct OutAccG {
   __device__ __forceinline__ void flush(uint32_t *gout) {
     const bool full = ab >= 32u;
     const uint32_t v = (uint32_t)acc;
-#ifdef MHQ_X_LONG_NOSTORE  // timing build: the streamed path's word stores skipped (wrong output)
-    if (false) {
-#else
     if (full && ow >= owf) {
-#endif
       CRUMB(53, gout + ow);
       if (!grouped(ow)) {
         if (DBG_OK(dbg_out_ok(gout + ow, 4), 23, gout + ow, ow)) gout[ow] = v;

@@ -151,11 +151,7 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu((kT / 64 * M
       __syncthreads();
       if (tid < m) sm.order[sm.hist[bk] + rk] = (uint16_t)tid;
       __syncthreads();
-#ifdef MHQ_X_ENC_NOWORK  // timing experiment only (wrong output): staging, sort and stores, no encoding
-      if (false) {
-#else
       if (tid < m) {
-#endif
         const uint32_t lit = sm.order[tid];
         const uint32_t r0 = sm.rec[lit], r1 = sm.rec[lit + 1];
         // an empty output region: the caller skips this literal (mhq_huff.h)
@@ -208,20 +204,13 @@ __device__ __forceinline__ uint32_t prow(uint32_t x) {
   return x < kRound ? x ^ ((x >> 2) & 0xcu) : x;
 }
 
-#ifndef MHQ_X_LEN  // timing experiments only (wrong output): 1 no byte loads, 2 no table lookups
-#define MHQ_X_LEN 0
-#endif
 __device__ __forceinline__ uint32_t chunk_bits(const u32x4 &x, const uint8_t *lens, uint32_t q[16]) {
   const uint32_t w[4] = {x.x, x.y, x.z, x.w};
   uint32_t t = 0;
 #pragma unroll
   for (int k = 0; k < 16; k++) {
     q[k] = t;
-#if MHQ_X_LEN & 2
-    t += (w[k >> 2] >> (8 * (k & 3))) & 0x7u;
-#else
     t += lens[(w[k >> 2] >> (8 * (k & 3))) & 0xffu];
-#endif
   }
   return t;
 }
@@ -293,11 +282,7 @@ __global__ __launch_bounds__(kLenThreads) void encode_len_kernel(const uint8_t *
       for (int k = 0; k < kLenRB; k++) {
         const uint64_t c = (uint64_t)(r0 + k) * kWave + lane;
         v[k] = u32x4{0u, 0u, 0u, 0u};
-#if !(MHQ_X_LEN & 1)  // (timing experiment 1: no byte loads)
         if (c < nchunk) v[k] = __builtin_nontemporal_load(src + c);  // aligned, holds a valid byte
-#else
-        v[k].x = (uint32_t)c;
-#endif
       }
 #pragma unroll
       for (int k = 0; k < kLenRB; k++) {

@@ -256,11 +256,7 @@ __device__ __forceinline__ void scan_apply_chunk(const F &f, uint64_t n, const u
   f.load(i0, a, b);
   const uint64_t first = (uint64_t)chunk * g;  // this chunk's first pair
   uint64_t pa = 0, pb = 0;
-#ifndef MHQ_X_SCAN  // timing experiments only (wrong output): 1 no prefix of the sums before the chunk, 2 no stores
-#define MHQ_X_SCAN 0
-#endif
-  if (MHQ_X_SCAN & 1) {
-  } else if (!sup) {
+  if (!sup) {
     // direct form (few sums, see direct_sums): the raw pairs before this
     // chunk's first, added up here; no second pass
     // (kDirectU loads per thread in flight at once: the pairs are L2 reads,
@@ -317,9 +313,7 @@ __device__ __forceinline__ void scan_apply_chunk(const F &f, uint64_t n, const u
   }
   typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
   const uint64_t c0 = (uint64_t)chunk * kChunk;
-  if (MHQ_X_SCAN & 2) {
-    if (xa[0] == 0x123456789ull) oa[0] = xb[kItems - 1];  // (keeps the values live)
-  } else if (c0 + kChunk <= n + 1) {
+  if (c0 + kChunk <= n + 1) {
     // a whole chunk: through LDS, so each wave-wide 16-B store covers 1 KiB
     // of consecutive offsets (stores straight from the owning threads touch
     // 64 lines each)

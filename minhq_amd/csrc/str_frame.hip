@@ -510,10 +510,8 @@ hipError_t launch_read_strings(const DevTables &t, const uint8_t *blk, uint64_t 
     }
     TRY(launch_read_fused(t, blk, blk_len, pos, limit, prefix, n, out, out_off, out_len, status, next, sc.start,
                           sc.hend, sc.kind, fallback, coop, gen, s));
-#ifndef MHQ_X_NOFB  // timing experiment only (no fallback: wrong for strings out of order)
     TRY(launch_read_fallback(t, blk, blk_len, pos, limit, prefix, n, out, out_cap, out_off, out_len, status, next,
                              sc.start, sc.hend, sc.kind, fallback, coop, coop + kReadFallbackMaxWgs, gen, s));
-#endif
     goto done;
   }
   read_parse_kernel<<<(unsigned)((n + kT * kParsePer - 1) / (kT * kParsePer)), kT, 0, s>>>(

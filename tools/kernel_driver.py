@@ -259,7 +259,7 @@ def main():
             s["st"] = torch.empty(n, dtype=torch.uint8, device=dev)
         elif args.kernel in ("encode", "encode_len", "layout", "packed"):
             s["in"], s["off"], s["eoff"] = data.clone(), off.clone(), enc_off.clone()
-            s["out"] = torch.empty((30 * b.nbytes + 7) // 8 if args.kernel == "packed" else enc_bytes + 16,
+            s["out"] = torch.empty(30 * b.nbytes // 8 + n if args.kernel == "packed" else enc_bytes + 16,
                                    dtype=torch.uint8, device=dev)
             s["len"] = torch.empty(n, dtype=torch.int32, device=dev)
             s["o1"] = torch.empty_like(enc_off)
