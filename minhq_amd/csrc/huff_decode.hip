@@ -73,6 +73,9 @@ __global__ __launch_bounds__(kT) void decode_kernel(const uint8_t *__restrict__ 
 #ifndef MHQ_DEC_LW_WORDS  // a lane's window in words (32: 128 B, 16: 64 B)
 #define MHQ_DEC_LW_WORDS 32
 #endif
+#ifndef MHQ_DEC_LW_PEND  // its output groups pending for wave-wide stores (OutAccGT)
+#define MHQ_DEC_LW_PEND 2
+#endif
 #ifndef MHQ_DEC_LW_BLOCKS  // its workgroups per CU
 #define MHQ_DEC_LW_BLOCKS 1
 #endif
@@ -110,8 +113,9 @@ __global__ __launch_bounds__(kLWaves * kWave, MHQ_DEC_LW_BLOCKS) void decode_lon
   while (tile < ntiles) {
     const uint64_t s = L0 + (uint64_t)tile * kWave;
     const uint32_t cnt = (uint32_t)min((uint64_t)kWave, L1 - s);
-    decode_tile_long_body<false, SmemL, LongWin, kLWords>(sm, sm.w[wave], in, in_off, nullptr, in_bias, out, out_off,
-                                                     out_bias, out_len, status, s, cnt, lane);
+    decode_tile_long_body<false, SmemL, LongWin, kLWords, MHQ_DEC_LW_PEND>(sm, sm.w[wave], in, in_off, nullptr,
+                                                                      in_bias, out, out_off, out_bias, out_len,
+                                                                      status, s, cnt, lane);
     uint32_t t = 0;
     if (lane == 0) t = atomicAdd(&sm.next_tile, 1u);
     tile = __builtin_amdgcn_readfirstlane(t);

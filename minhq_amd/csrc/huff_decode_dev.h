@@ -874,9 +874,23 @@ static_assert(sizeof(uint32_t) * kLongWords * kWave <= sizeof(uint32_t) * (kWIn 
 // word of a region that starts mid-word is shared with the previous
 // literal's region, so it is kept in `first` and finish() writes its bytes one
 // by one, as it does the decided bytes of the last word.
-struct OutAccG {
+// kPend (decode_long_kernel: 2): completed 16-B groups wait in up to kPend
+// slots (a third one in a round is stored at once) for drain(), which the
+// streamed loop calls for the whole wave right after a window refill: one
+// store instruction then carries most lanes' groups instead of the few lanes
+// that complete a group on a given step, and no store is in flight when the
+// next refill waits on vmcnt.  The stores cost config 5 31 % of the kernel
+// (1272 against 878 us without them; where they land made no difference,
+// profiles/r06/r06vx_*); this takes back 5 % (1274 -> 1211-1213 us; drains
+// every 8 steps instead: 1243; four slots: 1226).
+template <int kPend>
+struct OutAccGT {
+  static_assert(kPend >= 0 && kPend <= 4, "pending groups: up to four");
   uint64_t acc;
   uint32_t ow, ab, owf, first, rs, ga, q0, q1, q2, q3;
+  uint32_t np;
+  uint32_t pa[kPend > 0 ? kPend : 1];
+  u32x4 pg[kPend > 0 ? kPend : 1];  // (registers: indexed by constants only)
   // optr: the region's start from the 4-B aligned base gout; ga: gout's word
   // position in its 16-B group ((gout / 4) % 4), so word x sits at word
   // x + ga of the 16-B grid
@@ -889,6 +903,7 @@ struct OutAccG {
     first = 0;
     rs = optr;
     q0 = q1 = q2 = q3 = 0;
+    np = 0;
   }
   __device__ __forceinline__ void put(uint32_t syms, uint32_t nbits) {
     acc |= (uint64_t)syms << ab;
@@ -909,8 +924,17 @@ struct OutAccG {
         q1 = r == 1u ? v : q1;
         q2 = r == 2u ? v : q2;
         q3 = r == 3u ? v : q3;
-        if (r == 3u && DBG_OK(dbg_out_ok(gout + ow - 3u, 16), 24, gout + ow - 3u, ow))
+        if (kPend && r == 3u && np < (uint32_t)kPend) {  // (the group waits for drain)
+#pragma unroll
+          for (int k = 0; k < kPend; k++) {
+            const bool here = np == (uint32_t)k;
+            pg[k] = here ? u32x4{q0, q1, q2, v} : pg[k];
+            pa[k] = here ? ow - 3u : pa[k];
+          }
+          np++;
+        } else if (r == 3u && DBG_OK(dbg_out_ok(gout + ow - 3u, 16), 24, gout + ow - 3u, ow)) {
           *(u32x4 *)(gout + ow - 3u) = u32x4{q0, q1, q2, v};
+        }
       }
     }
     first = (full && ow < owf) ? v : first;
@@ -918,8 +942,17 @@ struct OutAccG {
     ow += ab >> 5;
     ab &= 31u;
   }
+  // the pending groups leave (the wave's lanes together)
+  __device__ __forceinline__ void drain(uint32_t *gout) {
+    if (!kPend) return;
+#pragma unroll
+    for (int k = 0; k < kPend; k++)
+      if (np > (uint32_t)k && DBG_OK(dbg_out_ok(gout + pa[k], 16), 24, gout + pa[k], pa[k])) *(u32x4 *)(gout + pa[k]) = pg[k];
+    np = 0;
+  }
   __device__ __forceinline__ void finish(uint32_t *gout) {
     flush(gout);
+    drain(gout);
     // whole words of the last, incomplete 16-B group
     CRUMB(54, gout + ow);
     if (grouped(ow)) {
@@ -942,12 +975,13 @@ struct OutAccG {
   }
   __device__ __forceinline__ uint32_t optr() const { return ow * 4u + (ab >> 3); }
 };
+using OutAccG = OutAccGT<0>;
 
 // The checked loop of decode_checked on a window, with the lane's running
 // accumulator (roomy literals only: no buffer-full rule).  Returns the status.
-template <class BB, class SM>
+template <class BB, class SM, class Acc>
 __device__ __forceinline__ uint32_t end_checked_g(const SM &sm, const uint32_t *win, uint32_t p, uint32_t endbit,
-                                                  OutAccG &out, uint32_t *gout, uint32_t swz) {
+                                                  Acc &out, uint32_t *gout, uint32_t swz) {
   BB in;
   in.init(win, p, swz);
   uint32_t bad = 0;
@@ -1011,7 +1045,7 @@ __device__ __forceinline__ void long_step(const SM &sm, uint32_t *otgt, BB &in, 
 // (decode_tile_long_body: always inlined -- the long-literal kernel's
 // register budget applies to it; decode_tile_long: the decode kernels' call,
 // inlined or not at the compiler's choice)
-template <bool kGaps, class SM, class W, uint32_t kW = kLongWords>
+template <bool kGaps, class SM, class W, uint32_t kW = kLongWords, int kPend = 0>
 __device__ __forceinline__ void decode_tile_long_body(const SM &sm, W &ws, const uint8_t *__restrict__ in,
                                  const uint64_t *__restrict__ in_off, const uint32_t *__restrict__ in_end,
                                  uint64_t in_bias, uint8_t *__restrict__ out,
@@ -1032,7 +1066,7 @@ __device__ __forceinline__ void decode_tile_long_body(const SM &sm, W &ws, const
   uint64_t ib = 0, ie = 0, ob = 0;
   uint64_t rel = 0;  // bits of the literal consumed
   uint32_t *gout = nullptr;
-  OutAccG acc;
+  OutAccGT<kPend> acc;
   acc.init(0);
   uint32_t ostart = 0;
   [[maybe_unused]] uint64_t oreg = 0;  // the literal's region (bytes; MHQ_DBG_BOUNDS)
@@ -1106,6 +1140,10 @@ __device__ __forceinline__ void decode_tile_long_body(const SM &sm, W &ws, const
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     wave_sync();
+    // the previous round's groups leave now that the window loads are in:
+    // stores issued just before a refill would hold up its vmcnt wait (gfx9
+    // counts stores in vmcnt), and one store carries most lanes' groups
+    acc.drain(gout);
     if (have) {
       const bool ends_here = endw + 64u <= kWinBits;
       BitBufS bin;
@@ -1117,8 +1155,8 @@ __device__ __forceinline__ void decode_tile_long_body(const SM &sm, W &ws, const
       // then single ones up to the end test's bound
       const int lim2 = lim0 - 30;
       while ((int)bin.p <= lim2 && lim != -1) {
-        long_step<OutAccG, BitBufS, false>(sm, gout, bin, acc, endw, lim, bad);
-        if (lim != -1) long_step<OutAccG, BitBufS, false>(sm, gout, bin, acc, endw, lim, bad);
+        long_step<OutAccGT<kPend>, BitBufS, false>(sm, gout, bin, acc, endw, lim, bad);
+        if (lim != -1) long_step<OutAccGT<kPend>, BitBufS, false>(sm, gout, bin, acc, endw, lim, bad);
         acc.flush(gout);
       }
       while ((int)bin.p <= lim) long_step(sm, gout, bin, acc, endw, lim, bad);
