@@ -150,6 +150,11 @@ __device__ __forceinline__ uint64_t wave_sum64(uint64_t v) {
   return v;
 }
 
+// Sum of a u32 over the 64 lanes of a full wave, in DPP moves (no LDS round
+// trips, unlike the shuffles of wave_sum64).
+__device__ __forceinline__ uint32_t wave_sum32(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_scan(v), kWave - 1);
+}
 
 // Totals (enc, cap) of workgroups [0, b), by ONE wave: lane l reads the
 // slots of workgroups b - 1 - l - 64 k (k < kLbW windows at once, spinning
@@ -204,8 +209,11 @@ __device__ bool look_back(const PackArgs &a, uint32_t b, uint32_t lane, uint64_t
       const uint32_t stop_e = me ? (uint32_t)__builtin_ctzll(me) : (uint32_t)kWave;
       const uint32_t stop_c = mc ? (uint32_t)__builtin_ctzll(mc) : (uint32_t)kWave;
       // the aggregates before the nearest inclusive prefix, and that prefix
-      const uint64_t xe = wave_sum64((!de && g >= 0 && lane <= stop_e) ? (uint32_t)ve[k] : 0u);
-      const uint64_t xc = wave_sum64((!dc && g >= 0 && lane <= stop_c) ? (uint32_t)vc[k] : 0u);
+      // (u32 sums in DPP moves: every sum of a batch's totals is < 2^32, see
+      // pack_slot; the 64-bit shuffle sums cost 72 LDS round trips a look-back:
+      // north star -0.5 us, profiles/r06/r06y_packed_lookback_dpp.txt)
+      const uint64_t xe = wave_sum32((!de && g >= 0 && lane <= stop_e) ? (uint32_t)ve[k] : 0u);
+      const uint64_t xc = wave_sum32((!dc && g >= 0 && lane <= stop_c) ? (uint32_t)vc[k] : 0u);
       se += xe;
       sc += xc;
       de = de || stop_e < (uint32_t)kWave;
