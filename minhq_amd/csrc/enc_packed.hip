@@ -19,9 +19,12 @@
 //   * enc_len, out_off and cap_off are written, and the staged plaintext is
 //     encoded into the zeroed output staging at the range's real alignment
 //     and stored with aligned 16-B stores.
-// A range whose plaintext or output exceeds the staging slices (a long
-// literal among short ones) is sized and encoded by one thread per literal
-// straight from global memory.  The look-back slots live in a buffer kept
+// A range whose plaintext exceeds the staging (longer literals among short
+// ones) is sized, then (after its look-back) encoded, in two halves staged one
+// after the other; a half that still overflows the plaintext or output
+// staging, and a staged range whose codes overflow the output staging, are
+// sized or encoded by one thread per literal straight from global memory.
+// The look-back slots live in a buffer kept
 // per caller stream for look-backs only (mhq_api.cpp), so a slot holds this
 // call's tag or an earlier call's, never another entry point's data; a
 // workgroup only waits for lower-numbered ones, which the dispatcher started
@@ -268,6 +271,36 @@ __device__ uint64_t size_literal_global(const uint8_t *src, uint64_t nbytes, con
   return bits;
 }
 
+// Stages the plaintext of literals [lo, hi) of the range at L0 (the pieces of
+// a range over the staging): in_w from the 16-B aligned start, rec[lo..hi]
+// their boundaries.  False, staging nothing, when the piece does not fit.
+// (uniform)
+template <int kPkIn, class SM>
+__device__ __forceinline__ bool stage_piece(SM &sm, const PackArgs &a, uint64_t L0, uint32_t lo, uint32_t hi,
+                                            uint32_t tid) {
+  const uint64_t pb = uniform64(vload(a.in_off, L0 + lo)), pe = uniform64(vload(a.in_off, L0 + hi));
+  const uint8_t *pa = a.in + (pb - a.in_bias);
+  const uint32_t pd = (uint32_t)((uintptr_t)pa & 15u);
+  if ((pe - pb) + pd > (uint64_t)kPkIn) return false;
+  const u32x4 *src = (const u32x4 *)(pa - pd);
+  const uint32_t chunks = pe > pb ? (uint32_t)(((pe - pb) + pd + 15u) >> 4) : 0u;
+  constexpr int kSC = (kPkIn / 16 + kT - 1) / kT;
+  u32x4 v4[kSC];
+#pragma unroll
+  for (int k = 0; k < kSC; k++) {
+    const uint32_t c = tid + (uint32_t)kT * k;
+    if (c < chunks) v4[k] = __builtin_nontemporal_load(src + c);  // aligned, holds a valid byte
+  }
+#pragma unroll
+  for (int k = 0; k < kSC; k++) {
+    const uint32_t c = tid + (uint32_t)kT * k;
+    if (c < chunks) *(u32x4 *)(sm.in_w + 4u * c) = v4[k];
+  }
+  if (tid == 0) sm.rec[lo] = (uint16_t)pd;
+  if (tid >= lo && tid < hi) sm.rec[tid + 1] = (uint16_t)((uint32_t)(a.in_off[L0 + tid + 1] - pb) + pd);
+  return true;
+}
+
 template <int kB>
 __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu((kT / 64 * kB + 3) / 4))) void encode_packed_kernel(
     PackArgs a, const uint32_t *__restrict__ g_code, const uint8_t *__restrict__ g_len) {
@@ -338,15 +371,28 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu((kT / 64 * k
     lit = tid < cnt ? sm.order[tid] : tid;
   }
   PKTL(b, 2, tid == 0);
-  if (tid < cnt) {
-    uint64_t bits;
-    if (staged) {
-      bits = encode_one<false>(sm, sm.rec[lit], sm.rec[lit + 1], 0u);
-    } else {
-      const uint64_t s0 = a.in_off[L0 + tid];
-      bits = size_literal_global(a.in + (s0 - a.in_bias), e_t - s0, sm.code);
+  if (staged) {
+    if (tid < cnt) sm.rel[lit] = (encode_one<false>(sm, sm.rec[lit], sm.rec[lit + 1], 0u) + 7u) >> 3;
+  } else {
+    // a range over the staging (long literals among short ones): its two
+    // halves are staged one after the other; a half that still overflows is
+    // sized a literal a thread from global memory
+    for (uint32_t q = 0; q < 2u; q++) {
+      const uint32_t lo = q ? cnt / 2u : 0u, hi = q ? cnt : cnt / 2u;
+      const bool pf = stage_piece<kPkIn>(sm, a, L0, lo, hi, tid);
+      __syncthreads();
+      if (tid >= lo && tid < hi) {
+        uint64_t bits;
+        if (pf) {
+          bits = encode_one<false>(sm, sm.rec[tid], sm.rec[tid + 1], 0u);
+        } else {
+          const uint64_t s0 = a.in_off[L0 + tid];
+          bits = size_literal_global(a.in + (s0 - a.in_bias), e_t - s0, sm.code);
+        }
+        sm.rel[tid] = (uint32_t)((bits + 7u) >> 3);
+      }
+      __syncthreads();  // (the next half's staging overwrites in_w and rec)
     }
-    sm.rel[lit] = (uint32_t)((bits + 7u) >> 3);
   }
   __syncthreads();
   PKTL(b, 3, tid == 0);
@@ -467,10 +513,44 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu((kT / 64 * k
   const uint32_t odelta = (uint32_t)((uintptr_t)oa & 15u);
   if (staged_out) {
     store_out_shifted(oa - odelta, sm.out_w, odelta, odelta + (uint32_t)min((uint64_t)T, room), odelta, tid, kT);
-  } else if (tid < cnt && v && rel_e + v <= room) {
-    const uint64_t s0 = a.in_off[L0 + tid];
-    const uint64_t e0 = a.in_off[L0 + tid + 1];  // (loaded again: e_t is not kept live across the look-back)
-    encode_literal_global<true>(a.in + (s0 - a.in_bias), e0 - s0, oa + rel_e, sm.code, nullptr);
+  } else if (staged) {  // the plaintext staged, its codes over the output staging
+    if (tid < cnt && v && rel_e + v <= room) {
+      const uint64_t s0 = a.in_off[L0 + tid];
+      const uint64_t e0 = a.in_off[L0 + tid + 1];  // (loaded again: e_t is not kept live across the look-back)
+      encode_literal_global<true>(a.in + (s0 - a.in_bias), e0 - s0, oa + rel_e, sm.code, nullptr);
+    }
+  } else {
+    // the two halves again, each staged, encoded into the output staging and
+    // stored at its place (rel_e of its first literal); a half whose
+    // plaintext or codes overflow is encoded a literal a thread from global
+    // memory
+    if (tid < cnt) sm.rel[tid] = rel_e;
+    for (uint32_t q = 0; q < 2u; q++) {
+      const uint32_t lo = q ? cnt / 2u : 0u, hi = q ? cnt : cnt / 2u;
+      __syncthreads();  // sm.rel complete; the previous half stored
+      const uint32_t r0 = __builtin_amdgcn_readfirstlane(lo < cnt ? sm.rel[lo] : T);
+      const uint32_t r1 = __builtin_amdgcn_readfirstlane(hi < cnt ? sm.rel[hi] : T);
+      const uint32_t tq = r1 - r0;
+      const bool pf = tq <= (uint32_t)kPkOut && stage_piece<kPkIn>(sm, a, L0, lo, hi, tid);
+      if (pf)
+        for (uint32_t c = tid; c < (tq + 15u) >> 4; c += kT) *(u32x4 *)(sm.out_w + 4u * c) = u32x4{0u, 0u, 0u, 0u};
+      __syncthreads();
+      if (tid >= lo && tid < hi && v) {
+        if (pf) {
+          encode_one<true>(sm, sm.rec[tid], sm.rec[tid + 1], rel_e - r0);
+        } else if (rel_e + v <= room) {
+          const uint64_t s0 = a.in_off[L0 + tid], e0 = a.in_off[L0 + tid + 1];
+          encode_literal_global<true>(a.in + (s0 - a.in_bias), e0 - s0, oa + rel_e, sm.code, nullptr);
+        }
+      }
+      __syncthreads();
+      if (pf) {
+        uint8_t *og = oa + r0;
+        const uint32_t od = (uint32_t)((uintptr_t)og & 15u);
+        const uint64_t rq = room > r0 ? room - r0 : 0u;
+        store_out_shifted(og - od, sm.out_w, od, od + (uint32_t)min((uint64_t)tq, rq), od, tid, kT);
+      }
+    }
   }
   PKTL(b, 8, tid == 0);
 }

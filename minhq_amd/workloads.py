@@ -80,6 +80,11 @@ def lengths(kind: str, n: int, seed: int, lo: int = 8, hi: int = 56) -> np.ndarr
         return (np.uint64(lo) + r % span).astype(np.int64)
     if kind == "fixed":
         return np.full(n, lo, dtype=np.int64)
+    if kind == "clustered":  # blocks of 512 literals alternating U{lo..hi} and U{8..lo} (the packed encode's ranges over and under its staging)
+        odd = (np.arange(n) // 512) % 2 == 1
+        a = np.uint64(lo) + r % np.uint64(hi - lo + 1)
+        b = np.uint64(8) + r % np.uint64(lo - 8 + 1)
+        return np.where(odd, b, a).astype(np.int64)
     if kind == "zipf":  # P(L=k) ~ 1/(k-3), k in 4..256
         ks = np.arange(4, 257)
         cdf = np.cumsum(1.0 / (ks - 3))

@@ -113,6 +113,35 @@ def test_packed_unstaged_ranges(codec, oracle_mod):
     _run(codec, oracle_mod, data, off)
 
 
+@pytest.mark.parametrize("shape", ["r512", "r448"])
+def test_packed_overflow_ranges_in_halves(codec, oracle_mod, shape):
+    """Ranges over the 20,224-B plaintext staging in batches whose mean keeps
+    the four-workgroup shape (512- and 448-literal ranges): each is sized and
+    encoded in two staged halves.  Both halves fit (blocks of 30-60-B
+    literals); only the second fits (a 15-KB literal in the first); the
+    plaintext fits but the codes overflow the 15,360-B output staging (random
+    bytes: 30-bit codes); empty literals throughout."""
+    from minhq_amd import hc, workloads as w
+
+    R = 512 if shape == "r512" else 448
+    rng = np.random.default_rng(49)
+    n = 24 * R
+    b = w.make_batch(n, "clustered", "hdr", 49, 30, 60) if shape == "r512" else \
+        w.make_batch(n, "uniform", "hdr", 49, 30, 46)
+    lits = hc.unpack(b.data, b.off)
+    for i in range(5 * R, 6 * R):  # both halves fit
+        lits[i] = bytes(rng.integers(97, 123, 58, dtype=np.uint8))
+    lits[9 * R + 3] = bytes(rng.integers(32, 127, 15000, dtype=np.uint8))  # the first half overflows
+    for i in range(13 * R, 14 * R):  # codes over the output staging
+        lits[i] = bytes(rng.integers(0, 256, 41, dtype=np.uint8))
+    for i in range(7, n, 89):
+        lits[i] = b""
+    data, off = hc.pack(lits)
+    mean = (off[-1] - off[0]) / n
+    assert (mean <= 37.5) == (shape == "r512") and mean <= 40, mean  # the shape under test
+    _run(codec, oracle_mod, data, off)
+
+
 def test_packed_staged_long_codes(codec, oracle_mod):
     """Short literals with a sprinkling of bytes whose codes exceed 24 bits
     (control and high bytes: the packed LDS table holds only the length for
