@@ -21,9 +21,10 @@
 //     and stored with aligned 16-B stores.
 // A range whose plaintext exceeds the staging (longer literals among short
 // ones) is sized, then (after its look-back) encoded, in two halves staged one
-// after the other; a half that still overflows the plaintext or output
-// staging, and a staged range whose codes overflow the output staging, are
-// sized or encoded by one thread per literal straight from global memory.
+// after the other; a staged range whose codes exceed the output staging
+// (printable text) is encoded in two halves too.  A half that still
+// overflows is sized or encoded by one thread per literal straight from
+// global memory.
 // The look-back slots live in a buffer kept
 // per caller stream for look-backs only (mhq_api.cpp), so a slot holds this
 // call's tag or an earlier call's, never another entry point's data; a
@@ -84,9 +85,9 @@ __device__ unsigned long long g_pktl[kPkWgs * kPkSlots];
 // staging (r05ax: config 2 -10 %, north star -7 %), ranges of kT literals
 // while such a range fits the staging and of kShortR = 448 above that, to the
 // packed route's 40-B bound (r05bh: -4 to -5 % against three workgroups with
-// 24 / 20 KB and 512-literal ranges; a range that overflows the staging takes
-// the slow per-literal global path: a 40-B mean in 512-literal ranges at four
-// ran 4.8x slower, r05bb).  The three-workgroup shape remains for means past
+// 24 / 20 KB and 512-literal ranges; a range that overflowed the staging then
+// took the per-literal global path: a 40-B mean in 512-literal ranges at four
+// ran 4.8x slower, r05bb; such ranges now go in staged halves, r06z).  The three-workgroup shape remains for means past
 // 42.9 B (none on the packed route) and MHQ_PK_SHORT_R=0 builds.
 #ifndef MHQ_PK_FOUR_RANGE_BYTES  // the four-workgroup shape up to this mean range of kT literals (bytes)
 #define MHQ_PK_FOUR_RANGE_BYTES 19200
@@ -513,17 +514,13 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu((kT / 64 * k
   const uint32_t odelta = (uint32_t)((uintptr_t)oa & 15u);
   if (staged_out) {
     store_out_shifted(oa - odelta, sm.out_w, odelta, odelta + (uint32_t)min((uint64_t)T, room), odelta, tid, kT);
-  } else if (staged) {  // the plaintext staged, its codes over the output staging
-    if (tid < cnt && v && rel_e + v <= room) {
-      const uint64_t s0 = a.in_off[L0 + tid];
-      const uint64_t e0 = a.in_off[L0 + tid + 1];  // (loaded again: e_t is not kept live across the look-back)
-      encode_literal_global<true>(a.in + (s0 - a.in_bias), e0 - s0, oa + rel_e, sm.code, nullptr);
-    }
   } else {
-    // the two halves again, each staged, encoded into the output staging and
-    // stored at its place (rel_e of its first literal); a half whose
-    // plaintext or codes overflow is encoded a literal a thread from global
-    // memory
+    // in two halves, each encoded into the output staging and stored at its
+    // place (rel_e of its first literal): a staged range whose codes overflow
+    // the output staging (printable text: ~1 code byte a byte), or a range
+    // over the plaintext staging, whose halves are staged again here; a half
+    // whose plaintext or codes overflow is encoded a literal a thread from
+    // global memory
     if (tid < cnt) sm.rel[tid] = rel_e;
     for (uint32_t q = 0; q < 2u; q++) {
       const uint32_t lo = q ? cnt / 2u : 0u, hi = q ? cnt : cnt / 2u;
@@ -531,7 +528,7 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu((kT / 64 * k
       const uint32_t r0 = __builtin_amdgcn_readfirstlane(lo < cnt ? sm.rel[lo] : T);
       const uint32_t r1 = __builtin_amdgcn_readfirstlane(hi < cnt ? sm.rel[hi] : T);
       const uint32_t tq = r1 - r0;
-      const bool pf = tq <= (uint32_t)kPkOut && stage_piece<kPkIn>(sm, a, L0, lo, hi, tid);
+      const bool pf = tq <= (uint32_t)kPkOut && (staged || stage_piece<kPkIn>(sm, a, L0, lo, hi, tid));
       if (pf)
         for (uint32_t c = tid; c < (tq + 15u) >> 4; c += kT) *(u32x4 *)(sm.out_w + 4u * c) = u32x4{0u, 0u, 0u, 0u};
       __syncthreads();
