@@ -199,6 +199,19 @@ def test_workload_labels():
     assert workloads.config5(64).name.startswith("config5-64x")
 
 
+def test_clustered_lengths():
+    """The `clustered` length kind (the packed encode's staged-halves timing
+    shape, tools/kernel_driver.py clustered:lo:hi): blocks of 512 literals
+    alternating U{lo..hi} and U{8..lo}."""
+    from minhq_amd import workloads
+
+    L = workloads.lengths("clustered", 4096, 7, 32, 60)
+    blocks = L.reshape(8, 512)
+    assert all(b.min() >= 32 and b.max() <= 60 for b in blocks[0::2])
+    assert all(b.min() >= 8 and b.max() <= 32 for b in blocks[1::2])
+    assert 31 < L.mean() < 35
+
+
 def test_table_driven_decoder_matches_restated(oracle_mod):
     """The table-driven CPU decoder (the honest CPU baseline beside the
     restated Go loop) gives the restated loop's results: valid
